@@ -1,0 +1,224 @@
+/*
+ * ecwide.h — C ABI of the MI355X wide-stripe erasure-coding engine.
+ *
+ * This is the drop-in boundary for ECWide-C's codec (`libcodec.so`,
+ * loaded by NativeCodec.java:213-215). Every entry point is plain C: raw
+ * pointers, sizes and int status codes; no torch or HIP types appear in a
+ * signature (streams are passed as `void*` = hipStream_t, NULL = default).
+ *
+ * Reference interface each function replaces (paths relative to the
+ * reference repository root):
+ *
+ *   ecw_scheme_from_ini       CodingScheme.getFromConfig   ECWide-C/src/CodingScheme.java:66-113
+ *   ecw_scheme_init           CodingScheme ctors           ECWide-C/src/CodingScheme.java:22-48
+ *   ecw_codec_create          NativeCodec ctors (R,T,L,C)  ECWide-C/src/NativeCodec.java:20-109
+ *                             + generateEncodeMatrix       ECWide-C/src/native/NativeCodec.cc:12-64
+ *                             + initEncodeTable            ECWide-C/src/native/NativeCodec.cc:66-88
+ *                             + initDecodeTable            ECWide-C/src/native/NativeCodec.cc:90-111
+ *                             + initPartialDecodeTable     ECWide-C/src/native/NativeCodec.cc:113-135
+ *   ecw_codec_encode_matrix   NativeCodec.getEncodeMatrix  ECWide-C/src/NativeCodec.java:127-131
+ *   ecw_codec_encode_gftbl    NativeCodec.getEncodeGftbl   ECWide-C/src/NativeCodec.java:133-137
+ *   ecw_codec_decode_gftbl    NativeCodec.getDecodeGftbl   ECWide-C/src/NativeCodec.java:139-143
+ *   ecw_encode                encodeData                   ECWide-C/src/native/NativeCodec.cc:137-219
+ *   ecw_decode                decodeData                   ECWide-C/src/native/NativeCodec.cc:221-249
+ *   ecw_partial_decode        partialDecodeData            ECWide-C/src/native/NativeCodec.cc:251-282
+ *   ecw_xor_intermediate      xorIntemediate               ECWide-C/src/native/NativeCodec.cc:284-323
+ *   ecw_*_dev                 the same operations on HBM-resident blocks (stream-ordered)
+ *   ecw_encode_batch_dev /    batches of independent stripes in one launch (north_star:
+ *   ecw_repair_batch_dev      "stripes are independent by byte range")
+ *   ecw_repair_sources        the flat fan-in of a CL single-block repair,
+ *                             ClMetadataManager.getChunkRepairTask  ECWide-C/src/ClMetadataManager.java:137-257
+ *
+ * Conventions (mirroring the reference):
+ *   - the caller owns every buffer; the library borrows pointers for the call;
+ *   - data arrives as arrays of per-block pointers (`const uint8_t* const*`);
+ *   - output order of encode is [G_0..G_{m-1}, L_0..L_{g-1}] (BufferUnit.java:60-68);
+ *   - unlike the reference (all void, nothing validated) every call validates
+ *     and returns an ecw_status; nothing calls exit();
+ *   - no static mutable state: all tables live in the codec; a codec may be
+ *     used from several host threads as long as each call uses its own
+ *     stream (host-pointer calls serialise on an internal per-codec lock).
+ */
+#ifndef ECWIDE_H_
+#define ECWIDE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ECW_ABI_VERSION 1
+
+typedef enum ecw_status {
+  ECW_OK = 0,
+  ECW_EINVAL = -1,       /* bad argument (null pointer, bad size, k+m > 256 ...) */
+  ECW_ENOMEM = -2,       /* host or device allocation failed */
+  ECW_EDEVICE = -3,      /* a HIP runtime call failed (no GPU, launch failure ...) */
+  ECW_EALIGN = -4,       /* device pointer / stride not 16-byte aligned */
+  ECW_EUNSUPPORTED = -5, /* operation the reference does not support either */
+  ECW_EPARSE = -6,       /* malformed scheme.ini */
+  ECW_EIO = -7           /* file could not be read */
+} ecw_status;
+
+/* Code types, same letters as NativeCodec.codeType (NativeCodec.java:9). */
+#define ECW_CODE_RS 'R'
+#define ECW_CODE_TL 'T'
+#define ECW_CODE_LRC 'L'
+#define ECW_CODE_CL 'C'
+
+/* Local-parity semantics of encode.
+ *  ECW_LOCAL_XOR     — L_t = XOR of group t's data blocks: the combined-locality
+ *                      code as designed (paper p.238), equal to ECWide-H
+ *                      l_encode (ECWide-H/proxy/encode.cpp:113-143) and to
+ *                      what decodeData assumes when it XORs a group back.
+ *  ECW_LOCAL_LITERAL — bit-exact with ECWide-C encodeData: its XOR table is
+ *                      built from an all-zero matrix (NativeCodec.cc:181-186),
+ *                      so every L block comes out 0x00.
+ * Global parities are identical in both modes. */
+#define ECW_LOCAL_XOR 0
+#define ECW_LOCAL_LITERAL 1
+
+/* xorIntemediate semantics.
+ *  ECW_XORI_XOR     — target[i] ^= source[i] on every call (the intent).
+ *  ECW_XORI_LITERAL — the reference's static `flag` is tested the wrong way
+ *                     round (NativeCodec.cc:287-292): the first call on a
+ *                     codec writes zeros into target, later calls XOR. */
+#define ECW_XORI_XOR 0
+#define ECW_XORI_LITERAL 1
+
+/* Scheme geometry (CodingScheme fields, CodingScheme.java:8-19). */
+typedef struct ecw_scheme {
+  char code_type;          /* 'R', 'T', 'L' or 'C' */
+  int k;                   /* data blocks */
+  int global_parity_num;   /* m (globalParityNum) */
+  int group_data_num;      /* r (groupDataNum), -1 for RS/TL */
+  int group_num;           /* ceil(k/r) for LRC/CL, 0 otherwise */
+  int rack_nodes_num;      /* m+1 (CL), m (TL), -1 (LRC), 0 (RS) */
+  int rack_num;            /* see CodingScheme ctors; -1 for LRC, 0 for RS */
+  int chunk_size_bits;     /* log2(chunk size) when parsed from ini, else -1 */
+  size_t chunk_size;       /* B, bytes per block */
+} ecw_scheme;
+
+/* Codec-derived counts (NativeCodec fields, NativeCodec.java:4-18). */
+typedef struct ecw_codec_info {
+  char code_type;
+  int node_index;
+  int multinode;
+  int local_mode;
+  int encode_data_num;     /* encodeDataNum */
+  int decode_data_num;     /* decodeDataNum */
+  int partial_decode_num;  /* partialDecodeNum (0 for RS/LRC) */
+  int global_num;          /* globalNum = m */
+  int group_num;           /* groupNum */
+  int group_data_num;      /* groupDataNum */
+  int rack_per_group;      /* rackPerGroup (CL only) */
+  int parity_num;          /* outputs of encode: m (+ groupNum for L/C) */
+  size_t chunk_size;
+} ecw_codec_info;
+
+typedef struct ecw_codec ecw_codec;
+
+/* ---- library ---------------------------------------------------------- */
+int ecw_abi_version(void);
+const char* ecw_status_string(int status);
+/* Number of visible HIP devices (0 on a host without GPU, never an error). */
+int ecw_device_count(void);
+
+/* ---- scheme ----------------------------------------------------------- */
+/* Build a scheme exactly as the CodingScheme constructors do. For RS/TL
+ * `group_data_num` is ignored. */
+int ecw_scheme_init(ecw_scheme* out, char code_type, int k, int m, int group_data_num,
+                    size_t chunk_size);
+/* Parse `codeType`, `k`, `groupDataNum`, `globalParityNum`, `chunkSizeBits`
+ * from a scheme.ini file (ECWide-C/config/scheme.ini), as
+ * CodingScheme.getFromConfig does. */
+int ecw_scheme_from_ini(const char* path, ecw_scheme* out);
+/* Same, from the file's text. */
+int ecw_scheme_from_ini_text(const char* text, ecw_scheme* out);
+
+/* ---- codec ------------------------------------------------------------ */
+/* Create a codec for `scheme` as seen from 1-based `node_index`.
+ * `multinode` selects the multi-node partial-encode geometry; only its
+ * counts are supported (encode with multinode=1 returns ECW_EUNSUPPORTED).
+ * `device` is the HIP device ordinal used for every device-side call;
+ * no device work happens until the first encode/decode call, so a codec can
+ * be created (and its matrices inspected) on a host without a GPU. */
+int ecw_codec_create(const ecw_scheme* scheme, int node_index, int multinode, int local_mode,
+                     int device, ecw_codec** out);
+void ecw_codec_destroy(ecw_codec* codec);
+int ecw_codec_get_info(const ecw_codec* codec, ecw_codec_info* out);
+int ecw_codec_set_xori_mode(ecw_codec* codec, int xori_mode);
+/* Copy out the m x k encode matrix (row-major), the 32*k*m ISA-L layout
+ * gf tables, and the 32*ddn / 32*pdn decode tables. `len` must equal the
+ * size the reference allocates (NativeCodec.java:101-104). */
+int ecw_codec_encode_matrix(const ecw_codec* codec, uint8_t* out, size_t len);
+int ecw_codec_encode_gftbl(const ecw_codec* codec, uint8_t* out, size_t len);
+int ecw_codec_decode_gftbl(const ecw_codec* codec, uint8_t* out, size_t len);
+int ecw_codec_partial_decode_gftbl(const ecw_codec* codec, uint8_t* out, size_t len);
+
+/* ---- host-memory entry points (blocking; mirror the JNI natives) -------
+ * `len` is the number of bytes per block (the reference always passes
+ * chunkSize; any len >= 0 is accepted). Each copies the inputs into HBM,
+ * runs the HIP kernels and copies the outputs back. */
+int ecw_encode(ecw_codec* codec, const uint8_t* const* data, uint8_t* const* parity, size_t len);
+int ecw_decode(ecw_codec* codec, const uint8_t* const* data, uint8_t* target, size_t len);
+int ecw_partial_decode(ecw_codec* codec, const uint8_t* const* data, uint8_t* target,
+                       size_t len);
+int ecw_xor_intermediate(ecw_codec* codec, const uint8_t* const* source, uint8_t* const* target,
+                         size_t len);
+
+/* ---- device-memory entry points (asynchronous on `stream`) -------------
+ * All pointers are HBM addresses, 16-byte aligned. The pointer arrays
+ * themselves are host arrays (copied into the kernel arguments). */
+int ecw_encode_dev(ecw_codec* codec, const uint8_t* const* d_data, uint8_t* const* d_parity,
+                   size_t len, void* stream);
+int ecw_decode_dev(ecw_codec* codec, const uint8_t* const* d_data, uint8_t* d_target,
+                   size_t len, void* stream);
+int ecw_partial_decode_dev(ecw_codec* codec, const uint8_t* const* d_data, uint8_t* d_target,
+                           size_t len, void* stream);
+int ecw_xor_intermediate_dev(ecw_codec* codec, const uint8_t* const* d_source,
+                             uint8_t* const* d_target, size_t len, void* stream);
+/* target = XOR of n device blocks (the arithmetic of decode / partial decode
+ * / relayer stage for any fan-in); n in [1, 256]. */
+int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* d_dst, size_t len,
+                       void* stream);
+
+/* ---- batched slab layout -----------------------------------------------
+ * A slab holds `stripes` stripes; stripe s starts at slab + s*stripe_stride,
+ * block b of a stripe at + b*block_stride. Block order inside a stripe is
+ * [D_0..D_{k-1}, G_0..G_{m-1}, L_0..L_{g-1}] (ChunkGenerator.java:51-103
+ * naming order). Strides must be multiples of 16; padding the block stride
+ * (e.g. B + 4 KiB) spreads the k concurrent row streams over HBM channels. */
+/* Encode every stripe of the slab: reads D blocks, writes G and L blocks. */
+int ecw_encode_batch_dev(ecw_codec* codec, uint8_t* d_slab, size_t block_stride,
+                         size_t stripe_stride, int stripes, size_t len, void* stream);
+/* Repair block `lost_block` (slab block index, D or L; G is "not yet" in the
+ * reference, ClMetadataManager.java:179-182) of every stripe into
+ * d_out + s*out_stride, as the XOR of its surviving group members. */
+int ecw_repair_batch_dev(ecw_codec* codec, const uint8_t* d_slab, size_t block_stride,
+                         size_t stripe_stride, int stripes, int lost_block, uint8_t* d_out,
+                         size_t out_stride, size_t len, void* stream);
+/* The slab block indices whose XOR rebuilds `lost_block` (a10: the r
+ * surviving members of its local group). Writes up to `cap` indices into
+ * `out_blocks`, returns the count (>0) or a negative ecw_status. */
+int ecw_repair_sources(const ecw_codec* codec, int lost_block, int* out_blocks, int cap);
+
+/* ---- synthetic data ------------------------------------------------------
+ * Counter-based generator used by tests and the bench (not part of the
+ * codec): byte i of block `block` of stripe `stripe` is byte (i % 8) of
+ *   w = mix64(key + (i/8) * 0x9E3779B97F4A7C15),
+ *   key = mix64(seed + 0x9E3779B97F4A7C15 * (1 + stripe * 65536 + block)),
+ * mix64 = splitmix64's finaliser. Fills `len` bytes of each of `nblocks`
+ * blocks (block index b0 + i at d_dst + i*block_stride) for every stripe
+ * s0 + s at + s*stripe_stride. */
+int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride,
+                        int stripes, int nblocks, size_t len, uint64_t seed, int s0, int b0,
+                        void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ECWIDE_H_ */

@@ -1,0 +1,443 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's hot path, used exclusively by tests/,
+ * __graft_entry__.smoke() and bench.py's cpu_baseline leg as the checker
+ * (never as the product path: the ecwide_amd library neither links nor
+ * loads this file).
+ *
+ * What is restated (paths relative to the reference root; `isal:` = file
+ * inside ECWide-H/isa-l-2.14.0.tar.gz, under isa-l-2.14.0/):
+ *   GF(2^8), poly 0x11D ............ isal:erasure_code/ec_base.c:36-60 (gf_mul, gf_inv)
+ *   gf_gen_rs_matrix ............... isal:erasure_code/ec_base.c:62-79
+ *   gf_gen_cauchy1_matrix .......... isal:erasure_code/ec_base.c:81-97
+ *   gf_vect_mul_init (32-B table) .. isal:erasure_code/ec_base.c:157-262
+ *   ec_init_tables ................. isal:erasure_code/ec_highlevel_func.c:33-43
+ *   ec_encode_data_base ............ isal:erasure_code/ec_base.c:290-305
+ *   ec_encode_data_avx2 dispatch ... isal:erasure_code/ec_highlevel_func.c:106-135
+ *     + gf_Nvect_dot_prod_avx2 ..... isal:erasure_code/gf_3vect_dot_prod_avx2.asm:293-380
+ *       (4-bit split vpshufb lookups; restated with intrinsics, same algorithm)
+ *   NativeCodec field derivations .. ECWide-C/src/NativeCodec.java:20-109,145-195
+ *   CodingScheme derivations ....... ECWide-C/src/CodingScheme.java:22-48
+ *   generateEncodeMatrix ........... ECWide-C/src/native/NativeCodec.cc:12-64 (single-node branch)
+ *   encodeData ..................... ECWide-C/src/native/NativeCodec.cc:137-219
+ *   decodeData / partialDecodeData . ECWide-C/src/native/NativeCodec.cc:221-282
+ *   xorIntemediate ................. ECWide-C/src/native/NativeCodec.cc:284-323
+ *
+ * Pinning: tests/golden/ holds vectors produced by oracle/_ref (ISA-L 2.14.0
+ * ec_base.c compiled from the reference tarball, see oracle/Makefile) and
+ * tests/test_oracle.py checks this file against them.
+ */
+#include <pthread.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
+
+/* ---------------- GF(2^8) ---------------- */
+static uint8_t g_exp[256], g_log[256];
+
+__attribute__((constructor)) static void orc_gf_build(void) {
+  unsigned x = 1;
+  for (int i = 0; i < 255; ++i) {
+    g_exp[i] = (uint8_t)x;
+    g_log[x] = (uint8_t)i;
+    x <<= 1;
+    if (x & 0x100) x ^= 0x11D;
+  }
+  g_exp[255] = g_exp[0];
+  g_log[0] = 0; /* unused: gf_mul tests for zero first */
+}
+
+uint8_t orc_gf_mul(uint8_t a, uint8_t b) {
+  if (a == 0 || b == 0) return 0;
+  int i = g_log[a] + g_log[b];
+  return g_exp[i > 254 ? i - 255 : i];
+}
+
+uint8_t orc_gf_inv(uint8_t a) {
+  if (a == 0) return 0;
+  return g_exp[255 - g_log[a]];
+}
+
+void orc_gen_rs_matrix(uint8_t* a, int m, int k) {
+  uint8_t gen = 1;
+  memset(a, 0, (size_t)k * m);
+  for (int i = 0; i < k; ++i) a[k * i + i] = 1;
+  for (int i = k; i < m; ++i) {
+    uint8_t p = 1;
+    for (int j = 0; j < k; ++j) {
+      a[k * i + j] = p;
+      p = orc_gf_mul(p, gen);
+    }
+    gen = orc_gf_mul(gen, 2);
+  }
+}
+
+void orc_gen_cauchy1_matrix(uint8_t* a, int m, int k) {
+  memset(a, 0, (size_t)k * m);
+  for (int i = 0; i < k; ++i) a[k * i + i] = 1;
+  uint8_t* p = a + (size_t)k * k;
+  for (int i = k; i < m; ++i)
+    for (int j = 0; j < k; ++j) *p++ = orc_gf_inv((uint8_t)(i ^ j));
+}
+
+/* tbl[0..15] = c*n, tbl[16..31] = c*(n<<4) */
+void orc_vect_mul_init(uint8_t c, uint8_t* tbl) {
+  for (int n = 0; n < 16; ++n) {
+    tbl[n] = orc_gf_mul(c, (uint8_t)n);
+    tbl[16 + n] = orc_gf_mul(c, (uint8_t)(n << 4));
+  }
+}
+
+void orc_init_tables(int k, int rows, const uint8_t* a, uint8_t* g_tbls) {
+  for (int i = 0; i < rows; ++i)
+    for (int j = 0; j < k; ++j) {
+      orc_vect_mul_init(*a++, g_tbls);
+      g_tbls += 32;
+    }
+}
+
+/* coefficient = v[..+1] (table entry c*1), as ec_encode_data_base reads it */
+void orc_encode_data_base(int len, int srcs, int dests, const uint8_t* v, uint8_t** src,
+                          uint8_t** dest) {
+  for (int l = 0; l < dests; ++l)
+    for (int i = 0; i < len; ++i) {
+      uint8_t s = 0;
+      for (int j = 0; j < srcs; ++j) s ^= orc_gf_mul(src[j][i], v[j * 32 + l * srcs * 32 + 1]);
+      dest[l][i] = s;
+    }
+}
+
+/* ---- AVX2 4-bit split port (the reference's actual CPU kernel family) ---- */
+#if defined(__x86_64__)
+__attribute__((target("avx2"))) static void dot_prod_avx2_rows(int len, int srcs, int rows,
+                                                                const uint8_t* v, uint8_t** src,
+                                                                uint8_t** dest) {
+  /* rows <= 6 outputs per pass, as gf_{1..6}vect_dot_prod_avx2 */
+  const __m256i mask = _mm256_set1_epi8(0x0f);
+  int pos = 0;
+  for (;;) {
+    if (pos > len - 32) {
+      if (pos == len) break;
+      pos = len - 32; /* overlapping last vector, as the asm does */
+    }
+    __m256i acc[6];
+    for (int l = 0; l < rows; ++l) acc[l] = _mm256_setzero_si256();
+    for (int j = 0; j < srcs; ++j) {
+      __m256i x = _mm256_loadu_si256((const __m256i*)(src[j] + pos));
+      __m256i lo = _mm256_and_si256(x, mask);
+      __m256i hi = _mm256_and_si256(_mm256_srli_epi64(x, 4), mask);
+      for (int l = 0; l < rows; ++l) {
+        const uint8_t* t = v + (size_t)l * srcs * 32 + (size_t)j * 32;
+        __m256i tl = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)t));
+        __m256i th = _mm256_broadcastsi128_si256(_mm_loadu_si128((const __m128i*)(t + 16)));
+        acc[l] = _mm256_xor_si256(acc[l], _mm256_xor_si256(_mm256_shuffle_epi8(tl, lo),
+                                                           _mm256_shuffle_epi8(th, hi)));
+      }
+    }
+    for (int l = 0; l < rows; ++l) _mm256_storeu_si256((__m256i*)(dest[l] + pos), acc[l]);
+    if (pos == len - 32) break;
+    pos += 32;
+  }
+}
+
+static int have_avx2(void) {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2");
+}
+#endif
+
+int orc_have_avx2(void) {
+#if defined(__x86_64__)
+  return have_avx2();
+#else
+  return 0;
+#endif
+}
+
+/* ec_encode_data_avx2 dispatch: len < 32 -> base; rows in passes of <= 4
+ * (gf_4vect first, then 3/2/1 for the remainder) */
+void orc_encode_data_avx2(int len, int srcs, int dests, const uint8_t* v, uint8_t** src,
+                          uint8_t** dest) {
+#if defined(__x86_64__)
+  if (len < 32 || !have_avx2()) {
+    orc_encode_data_base(len, srcs, dests, v, src, dest);
+    return;
+  }
+  while (dests >= 4) {
+    dot_prod_avx2_rows(len, srcs, 4, v, src, dest);
+    v += 4 * srcs * 32;
+    dest += 4;
+    dests -= 4;
+  }
+  if (dests > 0) dot_prod_avx2_rows(len, srcs, dests, v, src, dest);
+#else
+  orc_encode_data_base(len, srcs, dests, v, src, dest);
+#endif
+}
+
+/* ---------------- NativeCodec restatement ---------------- */
+typedef struct orc_codec {
+  /* CodingScheme */
+  char code_type;
+  int k, m, group_data_num, group_num, rack_nodes_num, rack_num;
+  int chunk_size;
+  /* NativeCodec */
+  int node_index, multinode;
+  int encode_data_num, decode_data_num, partial_decode_num, rack_per_group;
+  uint8_t* encode_matrix;   /* encode_data_num * m */
+  uint8_t* encode_gftbl;    /* 32 * edn * m */
+  uint8_t* decode_gftbl;    /* 32 * ddn */
+  uint8_t* partial_gftbl;   /* 32 * pdn */
+  int xori_called;          /* the reference's static `flag` (NativeCodec.cc:288) */
+} orc_codec;
+
+static int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+/* CodingScheme ctors (CodingScheme.java:22-48) */
+static void scheme_init(orc_codec* c, char t, int k, int m, int r, int chunk) {
+  c->code_type = t;
+  c->k = k;
+  c->m = m;
+  c->chunk_size = chunk;
+  c->group_data_num = -1;
+  c->group_num = 0;
+  c->rack_nodes_num = 0;
+  c->rack_num = 0;
+  if (t == 'T') {
+    c->rack_num = ceil_div(k, m) + 1;
+    c->rack_nodes_num = m;
+  } else if (t == 'L' || t == 'C') {
+    c->group_data_num = r;
+    c->group_num = ceil_div(k, r);
+    if (t == 'C') {
+      c->rack_nodes_num = m + 1;
+      c->rack_num = ceil_div(k + c->group_num, m + 1) + 1;
+    } else {
+      c->rack_nodes_num = c->rack_num = -1;
+    }
+  }
+}
+
+/* NativeCodec.getClPartialDecodeNum (NativeCodec.java:175-183) */
+static int cl_partial_decode_num(const orc_codec* c, int node) {
+  int rack = (node - 1) / c->rack_nodes_num;
+  if (rack != c->rack_num - 2) return c->rack_nodes_num;
+  int last = (c->k - 1) % c->group_data_num + 1;
+  return last % c->rack_nodes_num + 1;
+}
+
+/* NativeCodec.getTlPartialDecodeNum (NativeCodec.java:185-195) */
+static int tl_partial_decode_num(int k, int m, int node) {
+  int rn = m, rack = (node - 1) / rn, racks = ceil_div(k, m) + 1;
+  if (rack == racks - 2) {
+    int last = k - rack * rn;
+    return (last - 1) % rn + 1;
+  }
+  return rn;
+}
+
+void orc_codec_free(orc_codec* c) {
+  if (!c) return;
+  free(c->encode_matrix);
+  free(c->encode_gftbl);
+  free(c->decode_gftbl);
+  free(c->partial_gftbl);
+  free(c);
+}
+
+/* NativeCodec ctors (NativeCodec.java:20-109) + the four init natives. */
+orc_codec* orc_codec_new(char t, int k, int m, int r, int chunk, int node, int multinode) {
+  orc_codec* c = (orc_codec*)calloc(1, sizeof(orc_codec));
+  if (!c) return NULL;
+  scheme_init(c, t, k, m, r, chunk);
+  c->node_index = node;
+  c->multinode = multinode;
+  if (t == 'R') {
+    c->decode_data_num = c->encode_data_num = k;
+  } else if (t == 'T') {
+    int racks = ceil_div(k, m) + 1;
+    c->encode_data_num = k;
+    c->partial_decode_num = tl_partial_decode_num(k, m, node);
+    c->decode_data_num = c->partial_decode_num - 1 + racks - 1;
+  } else if (t == 'L') {
+    c->encode_data_num = k;
+    int gi = (node - 1) / r;
+    c->decode_data_num = (gi == r - 1) ? (k - 1) % r + 1 : r; /* sic, NativeCodec.java:63 */
+  } else { /* 'C' */
+    if (multinode)
+      c->encode_data_num = (node == 1) ? (k - 1) % r + 1 : r;
+    else
+      c->encode_data_num = k;
+    c->partial_decode_num = cl_partial_decode_num(c, node);
+    c->rack_per_group = ceil_div(r + 1, c->rack_nodes_num);
+    c->decode_data_num = c->partial_decode_num - 1 + c->rack_per_group - 1;
+  }
+  int edn = c->encode_data_num, ddn = c->decode_data_num, pdn = c->partial_decode_num;
+  c->encode_matrix = (uint8_t*)calloc((size_t)edn * m + 1, 1);
+  c->encode_gftbl = (uint8_t*)calloc((size_t)edn * m * 32 + 1, 1);
+  c->decode_gftbl = (uint8_t*)calloc((size_t)ddn * 32 + 1, 1);
+  c->partial_gftbl = (uint8_t*)calloc((size_t)pdn * 32 + 1, 1);
+  /* generateEncodeMatrix, single-node branch (NativeCodec.cc:31-34,59-61) */
+  int n = edn + m;
+  uint8_t* tmp = (uint8_t*)calloc((size_t)edn * n, 1);
+  orc_gen_cauchy1_matrix(tmp, n, edn);
+  memcpy(c->encode_matrix, tmp + (size_t)edn * edn, (size_t)edn * m);
+  free(tmp);
+  orc_init_tables(edn, m, c->encode_matrix, c->encode_gftbl);
+  uint8_t ones[256];
+  memset(ones, 1, sizeof ones);
+  orc_init_tables(ddn, 1, ones, c->decode_gftbl);
+  if (t == 'T' || t == 'C') orc_init_tables(pdn, 1, ones, c->partial_gftbl);
+  return c;
+}
+
+int orc_codec_field(const orc_codec* c, int which) {
+  switch (which) {
+    case 0: return c->encode_data_num;
+    case 1: return c->decode_data_num;
+    case 2: return c->partial_decode_num;
+    case 3: return c->group_num;
+    case 4: return c->rack_nodes_num;
+    case 5: return c->rack_num;
+    case 6: return c->rack_per_group;
+    case 7: return c->group_data_num;
+    default: return -1;
+  }
+}
+const uint8_t* orc_codec_matrix(const orc_codec* c) { return c->encode_matrix; }
+const uint8_t* orc_codec_gftbl(const orc_codec* c) { return c->encode_gftbl; }
+
+typedef void (*orc_ec_fn)(int, int, int, const uint8_t*, uint8_t**, uint8_t**);
+
+/* encodeData (NativeCodec.cc:137-219), single-node. `literal` reproduces
+ * the zero local-parity tables (NativeCodec.cc:181-186); otherwise the
+ * local tables are built from an all-ones row (the CL code as designed). */
+static void nc_encode(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
+                      orc_ec_fn ec, int off, int len) {
+  int k = c->encode_data_num, m = c->m;
+  uint8_t* d[256];
+  uint8_t* p[320];
+  for (int j = 0; j < k; ++j) d[j] = data[j] + off;
+  int np = m + ((c->code_type == 'C' || c->code_type == 'L') ? c->group_num : 0);
+  for (int i = 0; i < np; ++i) p[i] = parity[i] + off;
+  ec(len, k, m, c->encode_gftbl, d, p);
+  if (c->code_type != 'C' && c->code_type != 'L') return;
+  int r = c->group_data_num;
+  uint8_t row[256], *xor_tbl = (uint8_t*)malloc(32 * 256);
+  memset(row, literal ? 0 : 1, sizeof row);
+  orc_init_tables(r, 1, row, xor_tbl);
+  int pos = m, offset = 0;
+  for (int t = 0; t < c->group_num - 1; ++t, ++pos, offset += r) ec(len, r, 1, xor_tbl, d + offset, p + pos);
+  int last = (k - 1) % r + 1;
+  orc_init_tables(last, 1, row, xor_tbl);
+  ec(len, last, 1, xor_tbl, d + offset, p + pos);
+  free(xor_tbl);
+}
+
+void orc_nc_encode(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int avx2) {
+  nc_encode(c, data, parity, literal, avx2 ? orc_encode_data_avx2 : orc_encode_data_base, 0,
+            c->chunk_size);
+}
+
+void orc_nc_encode_len(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
+                       int avx2, int len) {
+  nc_encode(c, data, parity, literal, avx2 ? orc_encode_data_avx2 : orc_encode_data_base, 0, len);
+}
+
+/* decodeData / partialDecodeData: ec_encode_data with the all-ones table */
+void orc_nc_decode(const orc_codec* c, uint8_t** data, uint8_t* target, int len) {
+  uint8_t* t[1] = {target};
+  orc_encode_data_base(len, c->decode_data_num, 1, c->decode_gftbl, data, t);
+}
+void orc_nc_partial_decode(const orc_codec* c, uint8_t** data, uint8_t* target, int len) {
+  uint8_t* t[1] = {target};
+  orc_encode_data_base(len, c->partial_decode_num, 1, c->partial_gftbl, data, t);
+}
+
+/* xorIntemediate (NativeCodec.cc:284-323): first call -> zero tables */
+void orc_nc_xor_intermediate(orc_codec* c, uint8_t** src, uint8_t** tgt, int len, int literal) {
+  uint8_t tbl[64];
+  memset(tbl, 0, sizeof tbl);
+  if (!literal || c->xori_called) {
+    uint8_t a[2] = {1, 1};
+    orc_init_tables(2, 1, a, tbl);
+  }
+  for (int i = 0; i < c->m; ++i) {
+    uint8_t* d[2] = {src[i], tgt[i]};
+    uint8_t* o[1] = {tgt[i]};
+    orc_encode_data_base(len, 2, 1, tbl, d, o);
+  }
+  c->xori_called = 1;
+}
+
+/* ---- multi-threaded AVX2 baseline: the same flow split by byte range ---- */
+typedef struct {
+  const orc_codec* c;
+  uint8_t** data;
+  uint8_t** parity;
+  int literal, off, len;
+} mt_job;
+
+static void* mt_run(void* arg) {
+  mt_job* j = (mt_job*)arg;
+  nc_encode(j->c, j->data, j->parity, j->literal, orc_encode_data_avx2, j->off, j->len);
+  return NULL;
+}
+
+void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
+                      int nthreads, int len) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  pthread_t th[256];
+  mt_job jobs[256];
+  int per = (len / nthreads) & ~63;
+  if (per < 64) {
+    nc_encode(c, data, parity, literal, orc_encode_data_avx2, 0, len);
+    return;
+  }
+  for (int t = 0; t < nthreads; ++t) {
+    jobs[t].c = c;
+    jobs[t].data = data;
+    jobs[t].parity = parity;
+    jobs[t].literal = literal;
+    jobs[t].off = t * per;
+    jobs[t].len = (t == nthreads - 1) ? len - t * per : per;
+    pthread_create(&th[t], NULL, mt_run, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+}
+
+/* ---------------- synthetic data (ecwide.h, ecw_fill_random_dev) ---------------- */
+static uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+void orc_fill_random(uint8_t* dst, size_t len, uint64_t seed, uint32_t stripe, uint32_t block) {
+  const uint64_t G = 0x9E3779B97F4A7C15ull;
+  uint64_t key = mix64(seed + G * (1ull + (uint64_t)stripe * 65536ull + block));
+  size_t nw = len / 8;
+  for (size_t w = 0; w < nw; ++w) {
+    uint64_t v = mix64(key + (uint64_t)w * G);
+    memcpy(dst + 8 * w, &v, 8);
+  }
+  if (len % 8) {
+    uint64_t v = mix64(key + (uint64_t)nw * G);
+    memcpy(dst + 8 * nw, &v, len % 8);
+  }
+}
+
+/* XOR of n blocks (flat CL repair) */
+void orc_xor_blocks(uint8_t** src, int n, uint8_t* dst, size_t len) {
+  memset(dst, 0, len);
+  for (int i = 0; i < n; ++i)
+    for (size_t b = 0; b < len; ++b) dst[b] ^= src[i][b];
+}
