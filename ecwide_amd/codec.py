@@ -1,0 +1,267 @@
+"""Host-side mirror of ECWide-C's codec interface over the C ABI.
+
+``CodingScheme`` mirrors ECWide-C/src/CodingScheme.java and ``NativeCodec``
+mirrors ECWide-C/src/NativeCodec.java (same constructors/factories, field
+names and method names: ``encodeData``, ``decodeData``,
+``partialDecodeData``, ``xorIntemediate``). Buffers may be host numpy uint8
+arrays (the reference's direct ByteBuffers; blocking host entry points) or
+torch uint8 CUDA tensors resident in HBM (asynchronous device entry points on
+the current torch stream).
+
+Differences from the reference, all deliberate: every call validates its
+arguments and raises ``EcwError`` instead of crashing; no static state is
+shared between codecs; local parities are XOR by default (``local_mode``
+"literal" reproduces ECWide-C's all-zero L blocks, NativeCodec.cc:181-186).
+"""
+from __future__ import annotations
+
+import ctypes
+from ctypes import byref, c_int, c_void_p
+
+import numpy as np
+
+from . import _lib
+from ._lib import ecw_codec_info, ecw_scheme, lib
+
+LOCAL_MODES = {"xor": 0, "literal": 1}
+XORI_MODES = {"xor": 0, "literal": 1}
+
+
+class EcwError(RuntimeError):
+    def __init__(self, status: int, what: str):
+        self.status = status
+        super().__init__(f"{what}: {lib.ecw_status_string(status).decode()} ({status})")
+
+
+def _check(st: int, what: str) -> int:
+    if st < 0:
+        raise EcwError(st, what)
+    return st
+
+
+def _is_torch(x) -> bool:
+    return type(x).__module__.startswith("torch")
+
+
+def _addr(x) -> int:
+    if _is_torch(x):
+        if x.dtype.itemsize != 1 or not x.is_contiguous():
+            raise ValueError("device blocks must be contiguous uint8 tensors")
+        return x.data_ptr()
+    if not isinstance(x, np.ndarray) or x.dtype != np.uint8 or not x.flags["C_CONTIGUOUS"]:
+        raise ValueError("host blocks must be C-contiguous numpy uint8 arrays")
+    return x.ctypes.data
+
+
+def _nbytes(x) -> int:
+    return x.numel() if _is_torch(x) else x.size
+
+
+def _parr(bufs) -> ctypes.Array:
+    a = (c_void_p * max(1, len(bufs)))()
+    for i, b in enumerate(bufs):
+        a[i] = _addr(b)
+    return a
+
+
+def _on_device(bufs) -> bool:
+    kinds = {(_is_torch(b) and b.is_cuda) for b in bufs}
+    if len(kinds) != 1:
+        raise ValueError("mixing host and device blocks in one call")
+    return kinds.pop()
+
+
+def _stream():
+    import torch
+
+    return c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+class CodingScheme:
+    """CodingScheme.java: k, m/globalParityNum, groupDataNum, groupNum,
+    rackNodesNum, rackNum, chunkSize, codeType."""
+
+    CODES = {"RS": b"R", "TL": b"T", "LRC": b"L", "CL": b"C"}
+
+    def __init__(self, s: ecw_scheme):
+        self._s = s
+        self.codeType = {b"R": "RS", b"T": "TL", b"L": "LRC", b"C": "CL"}[s.code_type]
+        self.k = s.k
+        self.m = self.globalParityNum = s.global_parity_num
+        self.groupDataNum = s.group_data_num
+        self.groupNum = s.group_num
+        self.rackNodesNum = s.rack_nodes_num
+        self.rackNum = s.rack_num
+        self.chunkSize = s.chunk_size
+        self.chunkSizeBits = s.chunk_size_bits
+
+    @classmethod
+    def _make(cls, code: str, k: int, m: int, r: int, chunk: int) -> "CodingScheme":
+        s = ecw_scheme()
+        _check(lib.ecw_scheme_init(byref(s), cls.CODES[code], k, m, r, chunk), "CodingScheme")
+        return cls(s)
+
+    @classmethod
+    def getRsScheme(cls, k, m, chunkSize):
+        return cls._make("RS", k, m, -1, chunkSize)
+
+    @classmethod
+    def getTlScheme(cls, k, m, chunkSize):
+        return cls._make("TL", k, m, -1, chunkSize)
+
+    @classmethod
+    def getLrcScheme(cls, k, m, groupDataNum, chunkSize):
+        return cls._make("LRC", k, m, groupDataNum, chunkSize)
+
+    @classmethod
+    def getClScheme(cls, k, m, groupDataNum, chunkSize):
+        return cls._make("CL", k, m, groupDataNum, chunkSize)
+
+    @classmethod
+    def getFromConfig(cls, path: str) -> "CodingScheme":
+        s = ecw_scheme()
+        _check(lib.ecw_scheme_from_ini(str(path).encode(), byref(s)), f"getFromConfig({path})")
+        return cls(s)
+
+    @classmethod
+    def fromConfigText(cls, text: str) -> "CodingScheme":
+        s = ecw_scheme()
+        _check(lib.ecw_scheme_from_ini_text(text.encode(), byref(s)), "scheme.ini text")
+        return cls(s)
+
+    def __repr__(self):
+        return (f"CodingScheme({self.codeType}, k={self.k}, m={self.m}, r={self.groupDataNum}, "
+                f"chunkSize={self.chunkSize})")
+
+
+class NativeCodec:
+    """NativeCodec.java over libecwide.so."""
+
+    def __init__(self, scheme: CodingScheme, nodeIndex: int = 1, multiNodeEncode: bool = False,
+                 local_mode: str = "xor", device: int = 0):
+        h = c_void_p()
+        _check(lib.ecw_codec_create(byref(scheme._s), nodeIndex, int(multiNodeEncode),
+                                    LOCAL_MODES[local_mode], device, byref(h)), "NativeCodec")
+        self._h = h
+        self.scheme = scheme
+        self.device = device
+        info = ecw_codec_info()
+        _check(lib.ecw_codec_get_info(h, byref(info)), "info")
+        self.codeType = info.code_type.decode()
+        self.nodeIndex = info.node_index
+        self.multiNodeEncode = bool(info.multinode)
+        self.encodeDataNum = info.encode_data_num
+        self.decodeDataNum = info.decode_data_num
+        self.partialDecodeNum = info.partial_decode_num
+        self.globalNum = info.global_num
+        self.groupNum = info.group_num
+        self.groupDataNum = info.group_data_num
+        self.rackPerGroup = info.rack_per_group
+        self.parityNum = info.parity_num
+        self.chunkSize = info.chunk_size
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h:
+            lib.ecw_codec_destroy(h)
+            self._h = None
+
+    # -- factories (NativeCodec.java:111-125) --------------------------------
+    @classmethod
+    def getRsCodec(cls, scheme, **kw):
+        return cls(scheme, 1, False, **kw)
+
+    @classmethod
+    def getTlCodec(cls, scheme, nodeIndex, **kw):
+        return cls(scheme, nodeIndex, False, **kw)
+
+    @classmethod
+    def getLrcCodec(cls, scheme, nodeIndex, **kw):
+        return cls(scheme, nodeIndex, False, **kw)
+
+    @classmethod
+    def getClCodec(cls, scheme, nodeIndex, multiNodeEncode, **kw):
+        return cls(scheme, nodeIndex, multiNodeEncode, **kw)
+
+    # -- table getters (NativeCodec.java:127-143) ----------------------------
+    def _get(self, fn, n):
+        out = np.zeros(n, np.uint8)
+        _check(fn(self._h, out.ctypes.data_as(_lib._u8p), n), fn.__name__)
+        return out
+
+    def getEncodeMatrix(self) -> np.ndarray:
+        return self._get(lib.ecw_codec_encode_matrix, self.encodeDataNum * self.globalNum)
+
+    def getEncodeGftbl(self) -> np.ndarray:
+        return self._get(lib.ecw_codec_encode_gftbl, 32 * self.encodeDataNum * self.globalNum)
+
+    def getDecodeGftbl(self) -> np.ndarray:
+        return self._get(lib.ecw_codec_decode_gftbl, 32 * self.decodeDataNum)
+
+    def getPartialDecodeGftbl(self) -> np.ndarray:
+        return self._get(lib.ecw_codec_partial_decode_gftbl,
+                         32 * self.partialDecodeNum if self.codeType in "TC" else 0)
+
+    def setXorIntermediateMode(self, mode: str) -> None:
+        _check(lib.ecw_codec_set_xori_mode(self._h, XORI_MODES[mode]), "xori mode")
+
+    # -- the natives (NativeCodec.java:205-211) ------------------------------
+    def _len(self, bufs, length):
+        n = length if length is not None else min(_nbytes(b) for b in bufs)
+        return n
+
+    def encodeData(self, data, parity, length=None) -> None:
+        if len(data) < self.encodeDataNum or len(parity) < self.parityNum:
+            raise ValueError(f"need {self.encodeDataNum} data and {self.parityNum} parity blocks")
+        data, parity = list(data[:self.encodeDataNum]), list(parity[:self.parityNum])
+        n = self._len(data + parity, length)
+        if _on_device(data + parity):
+            _check(lib.ecw_encode_dev(self._h, _parr(data), _parr(parity), n, _stream()), "encodeData")
+        else:
+            _check(lib.ecw_encode(self._h, _parr(data), _parr(parity), n), "encodeData")
+
+    def decodeData(self, data, target, length=None) -> None:
+        data = list(data[:self.decodeDataNum])
+        if len(data) < self.decodeDataNum:
+            raise ValueError(f"need {self.decodeDataNum} blocks")
+        n = self._len(data + [target], length)
+        if _on_device(data + [target]):
+            _check(lib.ecw_decode_dev(self._h, _parr(data), _addr(target), n, _stream()), "decodeData")
+        else:
+            _check(lib.ecw_decode(self._h, _parr(data), _addr(target), n), "decodeData")
+
+    def partialDecodeData(self, data, target, length=None) -> None:
+        data = list(data[:self.partialDecodeNum])
+        if len(data) < self.partialDecodeNum:
+            raise ValueError(f"need {self.partialDecodeNum} blocks")
+        n = self._len(data + [target], length)
+        if _on_device(data + [target]):
+            _check(lib.ecw_partial_decode_dev(self._h, _parr(data), _addr(target), n, _stream()),
+                   "partialDecodeData")
+        else:
+            _check(lib.ecw_partial_decode(self._h, _parr(data), _addr(target), n), "partialDecodeData")
+
+    def xorIntemediate(self, source, target, length=None) -> None:
+        source, target = list(source[:self.globalNum]), list(target[:self.globalNum])
+        n = self._len(source + target, length)
+        if _on_device(source + target):
+            _check(lib.ecw_xor_intermediate_dev(self._h, _parr(source), _parr(target), n, _stream()),
+                   "xorIntemediate")
+        else:
+            _check(lib.ecw_xor_intermediate(self._h, _parr(source), _parr(target), n), "xorIntemediate")
+
+    # -- CL repair fan-in (ClMetadataManager.java:137-257, flattened) --------
+    def repairSources(self, lost_block: int) -> list:
+        buf = (c_int * 256)()
+        n = _check(lib.ecw_repair_sources(self._h, lost_block, buf, 256), "repairSources")
+        return list(buf[:n])
+
+
+def xor_reduce(src, dst, length=None, device: int = 0) -> None:
+    """dst = XOR of the device blocks in `src` (any fan-in 1..256)."""
+    n = length if length is not None else min(_nbytes(b) for b in list(src) + [dst])
+    _check(lib.ecw_xor_reduce_dev(device, _parr(list(src)), len(src), _addr(dst), n, _stream()), "xor_reduce")
+
+
+def device_count() -> int:
+    return lib.ecw_device_count()

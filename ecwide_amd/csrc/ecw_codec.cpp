@@ -1,0 +1,653 @@
+// Host side of the engine: scheme geometry, the codec object and every
+// C-ABI entry point declared in include/ecwide.h. The arithmetic itself runs
+// in the HIP kernels (ecw_kernels.hip); nothing here computes parity on the
+// CPU, and every device call fails loudly (ECW_EDEVICE) without a GPU.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cerrno>
+#include <climits>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <map>
+#include <mutex>
+#include <new>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "../../include/ecwide.h"
+#include "ecw_gf.hpp"
+#include "ecw_internal.hpp"
+
+using namespace ecw;
+
+namespace {
+
+int ceil_div(int a, int b) { return (a + b - 1) / b; }
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// Restores the caller's current device on scope exit (the C ABI must not
+// change thread state behind the caller's back).
+struct DeviceGuard {
+  int prev = -1;
+  bool ok = false;
+  explicit DeviceGuard(int dev) {
+    if (hipGetDevice(&prev) != hipSuccess) prev = -1;
+    ok = hipSetDevice(dev) == hipSuccess;
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+int status_of(hipError_t e) { return e == hipSuccess ? ECW_OK : ECW_EDEVICE; }
+
+}  // namespace
+
+struct ecw_codec {
+  ecw_scheme scheme{};
+  ecw_codec_info info{};
+  int device = 0;
+  int xori_mode = ECW_XORI_XOR;
+  std::vector<uint8_t> matrix;        // m x edn, row-major (encodeMatrix)
+  std::vector<uint8_t> gftbl;         // 32 * edn * m (encodeGftbl, ISA-L layout)
+  std::vector<uint8_t> dtbl, pdtbl;   // decode / partial-decode tables (all ones)
+  std::vector<std::vector<uint8_t>> pass_img;  // packed device tables per pass of <= 8 rows
+
+  std::mutex mu;                      // guards everything below
+  bool dev_ready = false;
+  std::vector<void*> d_pass;          // device copies of pass_img
+  bool xori_called = false;           // per-codec replacement of the static `flag`
+  // staging for the host-memory entry points
+  hipStream_t stream = nullptr;
+  uint8_t* d_stage = nullptr;
+  size_t stage_bytes = 0;
+
+  ~ecw_codec() {
+    if (dev_ready) {
+      DeviceGuard g(device);
+      for (void* p : d_pass) (void)hipFree(p);
+      if (d_stage) (void)hipFree(d_stage);
+      if (stream) (void)hipStreamDestroy(stream);
+    }
+  }
+
+  bool has_local() const { return info.code_type == 'C' || info.code_type == 'L'; }
+  int k() const { return info.encode_data_num; }
+  int m() const { return info.global_num; }
+  int groups() const { return has_local() ? info.group_num : 0; }
+  int r() const { return info.group_data_num; }
+
+  // lazily upload the packed tables (first device call)
+  int ensure_device() {
+    if (dev_ready) return ECW_OK;
+    DeviceGuard g(device);
+    if (!g.ok) return ECW_EDEVICE;
+    for (const auto& img : pass_img) {
+      void* p = nullptr;
+      if (hipMalloc(&p, img.size()) != hipSuccess) return ECW_ENOMEM;
+      if (hipMemcpy(p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
+        (void)hipFree(p);
+        return ECW_EDEVICE;
+      }
+      d_pass.push_back(p);
+    }
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return ECW_EDEVICE;
+    dev_ready = true;
+    return ECW_OK;
+  }
+
+  int ensure_stage(size_t bytes) {
+    if (stage_bytes >= bytes) return ECW_OK;
+    if (d_stage) (void)hipFree(d_stage);
+    d_stage = nullptr;
+    stage_bytes = 0;
+    if (hipMalloc(&d_stage, bytes) != hipSuccess) return ECW_ENOMEM;
+    stage_bytes = bytes;
+    return ECW_OK;
+  }
+};
+
+namespace {
+
+int local_mode_of(const ecw_codec* c) {
+  if (!c->has_local()) return kLocalNone;
+  return c->info.local_mode == ECW_LOCAL_LITERAL ? kLocalZero : kLocalXor;
+}
+
+// Encode through the kernels. `src(j)` / `dst(o)` give device row pointers for
+// pointer mode; for slab mode `slab` is set. Handles m > 8 (several passes),
+// m == 0 and > kMaxPtrLocals locals (XOR-reduce launches per group).
+struct EncodeTarget {
+  const uint8_t* const* src = nullptr;  // pointer mode
+  uint8_t* const* dst = nullptr;
+  const SlabRows* slab = nullptr;       // slab mode
+  int stripes = 1;
+};
+
+int run_encode(ecw_codec* c, const EncodeTarget& t, size_t len, hipStream_t s) {
+  const int k = c->k(), m = c->m(), ng = c->groups();
+  const int lmode = local_mode_of(c);
+  if (len == 0 || t.stripes == 0) return ECW_OK;
+  EncodeGeom g{};
+  g.len = len;
+  g.tiles = (len + kTileBytes - 1) / kTileBytes;
+  g.stripes = t.stripes;
+  g.k = k;
+  g.r = c->has_local() ? c->r() : k;
+  g.groups = ng;
+  g.m = m;
+  const int npass = (m + kMaxPassRows - 1) / kMaxPassRows;
+  // locals ride in the first pass when they fit in the pointer-mode args
+  const bool locals_inline = lmode != kLocalNone && m > 0 && (t.slab || ng <= kMaxPtrLocals);
+  for (int q = 0; q < npass; ++q) {
+    g.row0 = q * kMaxPassRows;
+    g.nrows = std::min(kMaxPassRows, m - g.row0);
+    g.local_mode = (q == 0 && locals_inline) ? lmode : kLocalNone;
+    hipError_t e;
+    if (t.slab) {
+      e = launch_encode_slab(*t.slab, g, c->d_pass[q], s);
+    } else {
+      PtrRows rows;
+      std::memset(&rows, 0, sizeof rows);
+      for (int j = 0; j < k; ++j) rows.src[j] = t.src[j];
+      for (int l = 0; l < g.nrows; ++l) rows.dst[l] = t.dst[g.row0 + l];
+      if (g.local_mode != kLocalNone)
+        for (int i = 0; i < ng; ++i) rows.dst[g.nrows + i] = t.dst[m + i];
+      e = launch_encode_ptr(rows, g, c->d_pass[q], s);
+    }
+    if (e != hipSuccess) return ECW_EDEVICE;
+  }
+  if (lmode != kLocalNone && !locals_inline) {
+    // m == 0 or very many local groups: one XOR reduce per group
+    for (int i = 0; i < ng; ++i) {
+      const int j0 = i * g.r, n = std::min(g.r, k - j0);
+      XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, t.stripes, n};
+      hipError_t e;
+      if (t.slab) {
+        XorSlab xs;
+        std::memset(&xs, 0, sizeof xs);
+        xs.base = t.slab->base;
+        xs.bstride = t.slab->bstride;
+        xs.sstride = t.slab->sstride;
+        xs.out = const_cast<uint8_t*>(t.slab->base) + static_cast<uint64_t>(k + m + i) * t.slab->bstride;
+        xs.ostride = t.slab->sstride;
+        for (int u = 0; u < n; ++u) xs.idx[u] = j0 + u;
+        if (lmode == kLocalZero) {
+          for (int st = 0; st < t.stripes; ++st)
+            if (hipMemsetAsync(xs.out + st * xs.ostride, 0, len, s) != hipSuccess) return ECW_EDEVICE;
+          continue;
+        }
+        e = launch_xor_slab(xs, xg, s);
+      } else {
+        if (lmode == kLocalZero) {
+          if (hipMemsetAsync(t.dst[m + i], 0, len, s) != hipSuccess) return ECW_EDEVICE;
+          continue;
+        }
+        XorPtr xp;
+        std::memset(&xp, 0, sizeof xp);
+        for (int u = 0; u < n; ++u) xp.src[u] = t.src[j0 + u];
+        xp.dst = t.dst[m + i];
+        e = launch_xor_ptr(xp, xg, s);
+      }
+      if (e != hipSuccess) return ECW_EDEVICE;
+    }
+  }
+  return ECW_OK;
+}
+
+int run_xor_ptr(const uint8_t* const* src, int n, uint8_t* dst, size_t len, hipStream_t s) {
+  if (n < 1 || n > kMaxSrc) return ECW_EINVAL;
+  if (len == 0) return ECW_OK;
+  XorPtr xp;
+  std::memset(&xp, 0, sizeof xp);
+  for (int i = 0; i < n; ++i) xp.src[i] = src[i];
+  xp.dst = dst;
+  XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, 1, n};
+  return status_of(launch_xor_ptr(xp, xg, s));
+}
+
+bool check_len(size_t len) { return len <= 0xFFFFFFF0ull; }
+
+template <class P>
+bool all_aligned(P const* ptrs, int n) {
+  for (int i = 0; i < n; ++i)
+    if (!ptrs[i] || !aligned16(ptrs[i])) return false;
+  return true;
+}
+
+}  // namespace
+
+// =====================================================================
+extern "C" {
+
+int ecw_abi_version(void) { return ECW_ABI_VERSION; }
+
+const char* ecw_status_string(int status) {
+  switch (status) {
+    case ECW_OK: return "ok";
+    case ECW_EINVAL: return "invalid argument";
+    case ECW_ENOMEM: return "out of memory";
+    case ECW_EDEVICE: return "HIP device error";
+    case ECW_EALIGN: return "pointer or stride not 16-byte aligned";
+    case ECW_EUNSUPPORTED: return "unsupported operation";
+    case ECW_EPARSE: return "malformed scheme.ini";
+    case ECW_EIO: return "file could not be read";
+    default: return "unknown status";
+  }
+}
+
+int ecw_device_count(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+// CodingScheme ctors (CodingScheme.java:22-48)
+int ecw_scheme_init(ecw_scheme* out, char code_type, int k, int m, int group_data_num, size_t chunk_size) {
+  if (!out) return ECW_EINVAL;
+  if (code_type != 'R' && code_type != 'T' && code_type != 'L' && code_type != 'C') return ECW_EINVAL;
+  if (k < 1 || m < 0 || k + m > 256) return ECW_EINVAL;
+  ecw_scheme s{};
+  s.code_type = code_type;
+  s.k = k;
+  s.global_parity_num = m;
+  s.chunk_size = chunk_size;
+  s.chunk_size_bits = -1;
+  s.group_data_num = -1;
+  if (code_type == 'T') {
+    if (m < 1) return ECW_EINVAL;
+    s.rack_num = ceil_div(k, m) + 1;
+    s.rack_nodes_num = m;
+  } else if (code_type == 'L' || code_type == 'C') {
+    if (group_data_num < 1) return ECW_EINVAL;
+    s.group_data_num = group_data_num;
+    s.group_num = ceil_div(k, group_data_num);
+    if (code_type == 'C') {
+      s.rack_nodes_num = m + 1;
+      s.rack_num = ceil_div(k + s.group_num, m + 1) + 1;
+    } else {
+      s.rack_nodes_num = s.rack_num = -1;
+    }
+  }
+  *out = s;
+  return ECW_OK;
+}
+
+// CodingScheme.getFromConfig (CodingScheme.java:66-113): "key = value" lines;
+// codeType CL/LRC/TL, anything else RS; the other values parseInt'ed.
+// Blank lines are skipped (the Java would throw on them); any other line
+// without '=' or with a non-integer value is ECW_EPARSE.
+int ecw_scheme_from_ini_text(const char* text, ecw_scheme* out) {
+  if (!text || !out) return ECW_EINVAL;
+  std::istringstream in(text);
+  std::string line;
+  std::map<std::string, long long> kv;
+  char code = 'C';
+  auto trim = [](std::string x) {
+    size_t a = 0, b = x.size();
+    while (a < b && std::isspace(static_cast<unsigned char>(x[a]))) ++a;
+    while (b > a && std::isspace(static_cast<unsigned char>(x[b - 1]))) --b;
+    return x.substr(a, b - a);
+  };
+  while (std::getline(in, line)) {
+    if (trim(line).empty()) continue;
+    const size_t eq = line.find('=');
+    if (eq == std::string::npos) return ECW_EPARSE;
+    const std::string key = trim(line.substr(0, eq));
+    std::string val = trim(line.substr(eq + 1));
+    const size_t eq2 = val.find('=');  // Java split("=")[1] drops the rest
+    if (eq2 != std::string::npos) val = trim(val.substr(0, eq2));
+    if (key == "codeType") {
+      code = val == "CL" ? 'C' : val == "LRC" ? 'L' : val == "TL" ? 'T' : 'R';
+      continue;
+    }
+    char* end = nullptr;
+    errno = 0;
+    const long long v = std::strtoll(val.c_str(), &end, 10);
+    if (val.empty() || *end != '\0' || errno || v < INT32_MIN || v > INT32_MAX) return ECW_EPARSE;
+    kv[key] = v;
+  }
+  for (const char* key : {"k", "chunkSizeBits", "globalParityNum"})
+    if (!kv.count(key)) return ECW_EPARSE;
+  if ((code == 'C' || code == 'L') && !kv.count("groupDataNum")) return ECW_EPARSE;
+  const long long bits = kv["chunkSizeBits"];
+  if (bits < 0 || bits > 31) return ECW_EPARSE;  // Java: 1 << bits on an int
+  const int r = (code == 'C' || code == 'L') ? static_cast<int>(kv["groupDataNum"]) : -1;
+  const int st = ecw_scheme_init(out, code, static_cast<int>(kv["k"]), static_cast<int>(kv["globalParityNum"]),
+                                 r, static_cast<size_t>(1) << bits);
+  if (st == ECW_OK) out->chunk_size_bits = static_cast<int>(bits);
+  return st;
+}
+
+int ecw_scheme_from_ini(const char* path, ecw_scheme* out) {
+  if (!path || !out) return ECW_EINVAL;
+  std::ifstream f(path);
+  if (!f) return ECW_EIO;
+  std::stringstream ss;
+  ss << f.rdbuf();
+  const std::string text = ss.str();
+  return ecw_scheme_from_ini_text(text.c_str(), out);
+}
+
+// NativeCodec ctors (NativeCodec.java:20-109) and the four init natives
+// (NativeCodec.cc:12-135).
+int ecw_codec_create(const ecw_scheme* sch, int node_index, int multinode, int local_mode, int device,
+                     ecw_codec** out) {
+  if (!sch || !out) return ECW_EINVAL;
+  *out = nullptr;
+  if (local_mode != ECW_LOCAL_XOR && local_mode != ECW_LOCAL_LITERAL) return ECW_EINVAL;
+  const char t = sch->code_type;
+  const int k = sch->k, m = sch->global_parity_num, r = sch->group_data_num;
+  if (k < 1 || m < 0 || k + m > 256) return ECW_EINVAL;
+  if ((t == 'C' || t == 'L') && (r < 1 || sch->rack_nodes_num == 0)) return ECW_EINVAL;
+  if ((t == 'T' || t == 'C') && node_index < 1) return ECW_EINVAL;
+  if (t == 'L' && node_index < 1) return ECW_EINVAL;
+  if (multinode && t != 'C') return ECW_EINVAL;
+  ecw_codec* c = new (std::nothrow) ecw_codec();
+  if (!c) return ECW_ENOMEM;
+  c->scheme = *sch;
+  c->device = device;
+  ecw_codec_info& in = c->info;
+  in.code_type = t;
+  in.node_index = node_index;
+  in.multinode = multinode ? 1 : 0;
+  in.local_mode = local_mode;
+  in.global_num = m;
+  in.chunk_size = sch->chunk_size;
+  in.group_num = sch->group_num;
+  in.group_data_num = sch->group_data_num;
+  if (t == 'R') {
+    in.decode_data_num = in.encode_data_num = k;
+  } else if (t == 'T') {
+    const int racks = ceil_div(k, m) + 1, rn = m, rack = (node_index - 1) / rn;
+    in.encode_data_num = k;
+    in.partial_decode_num = rack == racks - 2 ? ((k - rack * rn) - 1) % rn + 1 : rn;
+    in.decode_data_num = in.partial_decode_num - 1 + racks - 1;
+  } else if (t == 'L') {
+    in.encode_data_num = k;
+    const int gi = (node_index - 1) / r;
+    in.decode_data_num = gi == r - 1 ? (k - 1) % r + 1 : r;  // sic: NativeCodec.java:63
+  } else {
+    in.encode_data_num = multinode ? (node_index == 1 ? (k - 1) % r + 1 : r) : k;
+    const int rn = sch->rack_nodes_num, rack = (node_index - 1) / rn;
+    in.partial_decode_num = rack != sch->rack_num - 2 ? rn : ((k - 1) % r + 1) % rn + 1;
+    in.rack_per_group = ceil_div(r + 1, rn);
+    in.decode_data_num = in.partial_decode_num - 1 + in.rack_per_group - 1;
+  }
+  in.parity_num = m + ((t == 'C' || t == 'L') ? in.group_num : 0);
+  const int edn = in.encode_data_num;
+  c->matrix = cauchy_parity_rows(edn, m);
+  c->gftbl = isal_tables(edn, m, c->matrix.data());
+  std::vector<uint8_t> ones(256, 1);
+  c->dtbl = isal_tables(in.decode_data_num, 1, ones.data());
+  if (t == 'T' || t == 'C') c->pdtbl = isal_tables(in.partial_decode_num, 1, ones.data());
+  for (int row0 = 0; row0 < m; row0 += kMaxPassRows)
+    c->pass_img.push_back(packed_pass_tables(c->matrix.data(), edn, row0, std::min(kMaxPassRows, m - row0)));
+  *out = c;
+  return ECW_OK;
+}
+
+void ecw_codec_destroy(ecw_codec* codec) { delete codec; }
+
+int ecw_codec_get_info(const ecw_codec* c, ecw_codec_info* out) {
+  if (!c || !out) return ECW_EINVAL;
+  *out = c->info;
+  return ECW_OK;
+}
+
+int ecw_codec_set_xori_mode(ecw_codec* c, int mode) {
+  if (!c || (mode != ECW_XORI_XOR && mode != ECW_XORI_LITERAL)) return ECW_EINVAL;
+  std::lock_guard<std::mutex> lk(c->mu);
+  c->xori_mode = mode;
+  return ECW_OK;
+}
+
+static int copy_out(const std::vector<uint8_t>& v, uint8_t* out, size_t len) {
+  if (!out || len != v.size()) return ECW_EINVAL;
+  if (len) std::memcpy(out, v.data(), len);
+  return ECW_OK;
+}
+int ecw_codec_encode_matrix(const ecw_codec* c, uint8_t* out, size_t len) {
+  return c ? copy_out(c->matrix, out, len) : ECW_EINVAL;
+}
+int ecw_codec_encode_gftbl(const ecw_codec* c, uint8_t* out, size_t len) {
+  return c ? copy_out(c->gftbl, out, len) : ECW_EINVAL;
+}
+int ecw_codec_decode_gftbl(const ecw_codec* c, uint8_t* out, size_t len) {
+  return c ? copy_out(c->dtbl, out, len) : ECW_EINVAL;
+}
+int ecw_codec_partial_decode_gftbl(const ecw_codec* c, uint8_t* out, size_t len) {
+  return c ? copy_out(c->pdtbl, out, len) : ECW_EINVAL;
+}
+
+// ---- device entry points ----------------------------------------------------
+int ecw_encode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* const* d_parity, size_t len,
+                   void* stream) {
+  if (!c || !d_data || !d_parity || !check_len(len)) return ECW_EINVAL;
+  if (c->info.multinode) return ECW_EUNSUPPORTED;
+  const int k = c->k(), np = c->info.parity_num;
+  if (!all_aligned(d_data, k) || !all_aligned(d_parity, np)) return ECW_EALIGN;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int st = c->ensure_device();
+    if (st) return st;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  EncodeTarget t;
+  t.src = d_data;
+  t.dst = d_parity;
+  return run_encode(c, t, len, static_cast<hipStream_t>(stream));
+}
+
+int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* d_dst, size_t len, void* stream) {
+  if (!d_src || !d_dst || n < 1 || n > kMaxSrc || !check_len(len)) return ECW_EINVAL;
+  if (!all_aligned(d_src, n) || !aligned16(d_dst)) return ECW_EALIGN;
+  DeviceGuard g(device);
+  if (!g.ok) return ECW_EDEVICE;
+  return run_xor_ptr(d_src, n, d_dst, len, static_cast<hipStream_t>(stream));
+}
+
+int ecw_decode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* d_target, size_t len, void* stream) {
+  if (!c) return ECW_EINVAL;
+  return ecw_xor_reduce_dev(c->device, d_data, c->info.decode_data_num, d_target, len, stream);
+}
+
+int ecw_partial_decode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* d_target, size_t len,
+                           void* stream) {
+  if (!c) return ECW_EINVAL;
+  if (c->info.partial_decode_num < 1) return ECW_EUNSUPPORTED;  // RS/LRC codecs have no partial decode
+  return ecw_xor_reduce_dev(c->device, d_data, c->info.partial_decode_num, d_target, len, stream);
+}
+
+int ecw_xor_intermediate_dev(ecw_codec* c, const uint8_t* const* d_src, uint8_t* const* d_tgt, size_t len,
+                             void* stream) {
+  if (!c || !d_src || !d_tgt || !check_len(len)) return ECW_EINVAL;
+  const int m = c->m();
+  if (!all_aligned(d_src, m) || !all_aligned(d_tgt, m)) return ECW_EALIGN;
+  bool zero_first;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    zero_first = c->xori_mode == ECW_XORI_LITERAL && !c->xori_called;
+    c->xori_called = true;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  for (int i = 0; i < m; ++i) {
+    if (zero_first) {
+      if (len && hipMemsetAsync(d_tgt[i], 0, len, s) != hipSuccess) return ECW_EDEVICE;
+      continue;
+    }
+    const uint8_t* two[2] = {d_src[i], d_tgt[i]};
+    const int st = run_xor_ptr(two, 2, d_tgt[i], len, s);
+    if (st) return st;
+  }
+  return ECW_OK;
+}
+
+int ecw_encode_batch_dev(ecw_codec* c, uint8_t* d_slab, size_t block_stride, size_t stripe_stride, int stripes,
+                         size_t len, void* stream) {
+  if (!c || !d_slab || stripes < 0 || !check_len(len) || len > block_stride) return ECW_EINVAL;
+  if (c->info.multinode) return ECW_EUNSUPPORTED;
+  if (!aligned16(d_slab) || block_stride % 16 || stripe_stride % 16) return ECW_EALIGN;
+  const size_t nblk = static_cast<size_t>(c->k()) + c->info.parity_num;
+  if (stripes > 1 && stripe_stride < nblk * block_stride) return ECW_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int st = c->ensure_device();
+    if (st) return st;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  SlabRows slab{d_slab, block_stride, stripe_stride};
+  EncodeTarget t;
+  t.slab = &slab;
+  t.stripes = stripes;
+  return run_encode(c, t, len, static_cast<hipStream_t>(stream));
+}
+
+// a10: flat CL single-block repair = XOR of the surviving members of the lost
+// block's local group (ClMetadataManager.java:161-183 takes the group's
+// positions; XOR is associative, so the two-stage relay of
+// ECTaskProcessor.java:293-332 gives the identical bytes).
+int ecw_repair_sources(const ecw_codec* c, int lost, int* out, int cap) {
+  if (!c || !out) return ECW_EINVAL;
+  if (!c->has_local() || c->info.multinode) return ECW_EUNSUPPORTED;
+  const int k = c->k(), m = c->m(), r = c->r(), ng = c->groups();
+  if (lost < 0 || lost >= k + m + ng) return ECW_EINVAL;
+  if (lost >= k && lost < k + m) return ECW_EUNSUPPORTED;  // G repair: "not yet" (ClMetadataManager.java:179-182)
+  const int t = lost < k ? lost / r : lost - k - m;
+  const int j0 = t * r, n = std::min(r, k - j0);
+  if (cap < n) return ECW_EINVAL;
+  int w = 0;
+  for (int j = j0; j < j0 + n; ++j)
+    if (j != lost) out[w++] = j;
+  if (lost < k) out[w++] = k + m + t;  // the group's local parity
+  return w;
+}
+
+int ecw_repair_batch_dev(ecw_codec* c, const uint8_t* d_slab, size_t block_stride, size_t stripe_stride,
+                         int stripes, int lost_block, uint8_t* d_out, size_t out_stride, size_t len, void* stream) {
+  if (!c || !d_slab || !d_out || stripes < 0 || !check_len(len) || len > block_stride) return ECW_EINVAL;
+  if (!aligned16(d_slab) || !aligned16(d_out) || block_stride % 16 || stripe_stride % 16 || out_stride % 16)
+    return ECW_EALIGN;
+  if (c->info.local_mode == ECW_LOCAL_LITERAL) return ECW_EUNSUPPORTED;  // literal L blocks are zeros
+  XorSlab xs;
+  std::memset(&xs, 0, sizeof xs);
+  const int n = ecw_repair_sources(c, lost_block, xs.idx, kMaxSrc);
+  if (n < 0) return n;
+  if (n == 0) return ECW_EUNSUPPORTED;
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  xs.base = d_slab;
+  xs.bstride = block_stride;
+  xs.sstride = stripe_stride;
+  xs.out = d_out;
+  xs.ostride = out_stride;
+  XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
+  if (len == 0 || stripes == 0) return ECW_OK;
+  return status_of(launch_xor_slab(xs, xg, static_cast<hipStream_t>(stream)));
+}
+
+int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride, int stripes,
+                        int nblocks, size_t len, uint64_t seed, int s0, int b0, void* stream) {
+  if (!d_dst || stripes < 0 || nblocks < 0 || s0 < 0 || b0 < 0) return ECW_EINVAL;
+  if (nblocks > 1 && block_stride < len) return ECW_EINVAL;
+  if (!aligned16(d_dst) || block_stride % 16 || stripe_stride % 16) return ECW_EALIGN;
+  DeviceGuard g(device);
+  if (!g.ok) return ECW_EDEVICE;
+  return status_of(launch_fill_random(d_dst, block_stride, stripe_stride, stripes, nblocks, len, seed, s0, b0,
+                                      static_cast<hipStream_t>(stream)));
+}
+
+// ---- host-memory entry points (blocking) ------------------------------------
+// Inputs are copied into a per-codec HBM staging area, the kernels run, the
+// outputs come back. Serialised per codec (the staging area is shared).
+static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8_t* const* out, int nout,
+                          size_t len, int (*op)(ecw_codec*, uint8_t* const*, int, uint8_t* const*, int, size_t,
+                                                hipStream_t)) {
+  for (int i = 0; i < nin; ++i)
+    if (!in[i]) return ECW_EINVAL;
+  for (int i = 0; i < nout; ++i)
+    if (!out[i]) return ECW_EINVAL;
+  if (len == 0) return ECW_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int st = c->ensure_device();
+  if (st) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  const size_t stride = (len + 255) & ~static_cast<size_t>(255);
+  st = c->ensure_stage(stride * (nin + nout));
+  if (st) return st;
+  std::vector<uint8_t*> din(nin), dout(nout);
+  for (int i = 0; i < nin; ++i) din[i] = c->d_stage + i * stride;
+  for (int i = 0; i < nout; ++i) dout[i] = c->d_stage + (nin + i) * stride;
+  for (int i = 0; i < nin; ++i)
+    if (hipMemcpyAsync(din[i], in[i], len, hipMemcpyHostToDevice, c->stream) != hipSuccess) return ECW_EDEVICE;
+  st = op(c, din.data(), nin, dout.data(), nout, len, c->stream);
+  if (st) return st;
+  for (int i = 0; i < nout; ++i)
+    if (hipMemcpyAsync(out[i], dout[i], len, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return ECW_EDEVICE;
+  return hipStreamSynchronize(c->stream) == hipSuccess ? ECW_OK : ECW_EDEVICE;
+}
+
+static int op_encode(ecw_codec* c, uint8_t* const* din, int, uint8_t* const* dout, int, size_t len, hipStream_t s) {
+  EncodeTarget t;
+  t.src = din;
+  t.dst = dout;
+  return run_encode(c, t, len, s);
+}
+static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout, int, size_t len, hipStream_t s) {
+  return run_xor_ptr(din, nin, dout[0], len, s);
+}
+
+int ecw_encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
+  if (!c || !data || !parity || !check_len(len)) return ECW_EINVAL;
+  if (c->info.multinode) return ECW_EUNSUPPORTED;
+  return host_roundtrip(c, data, c->k(), parity, c->info.parity_num, len, op_encode);
+}
+
+int ecw_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target, size_t len) {
+  if (!c || !data || !target || !check_len(len)) return ECW_EINVAL;
+  uint8_t* const out[1] = {target};
+  return host_roundtrip(c, data, c->info.decode_data_num, out, 1, len, op_xor);
+}
+
+int ecw_partial_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target, size_t len) {
+  if (!c || !data || !target || !check_len(len)) return ECW_EINVAL;
+  if (c->info.partial_decode_num < 1) return ECW_EUNSUPPORTED;
+  uint8_t* const out[1] = {target};
+  return host_roundtrip(c, data, c->info.partial_decode_num, out, 1, len, op_xor);
+}
+
+int ecw_xor_intermediate(ecw_codec* c, const uint8_t* const* source, uint8_t* const* target, size_t len) {
+  if (!c || !source || !target || !check_len(len)) return ECW_EINVAL;
+  const int m = c->m();
+  bool zero_first;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    zero_first = c->xori_mode == ECW_XORI_LITERAL && !c->xori_called;
+    c->xori_called = true;
+  }
+  for (int i = 0; i < m; ++i) {
+    if (!source[i] || !target[i]) return ECW_EINVAL;
+    if (zero_first) {
+      std::memset(target[i], 0, len);  // the reference's first-call output (NativeCodec.cc:287-292)
+      continue;
+    }
+    const uint8_t* in[2] = {source[i], target[i]};
+    uint8_t* const out[1] = {target[i]};
+    const int st = host_roundtrip(c, in, 2, out, 1, len, op_xor);
+    if (st) return st;
+  }
+  return ECW_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,75 @@
+// Internal interface between the host codec (ecw_codec.cpp) and the HIP
+// kernels (ecw_kernels.hip). Not part of the C ABI.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+namespace ecw {
+
+constexpr int kMaxSrc = 256;      // k + m <= 256 for a GF(2^8) Cauchy code
+constexpr int kMaxPassRows = 8;   // global rows per encode pass (u64 packed entries)
+constexpr int kMaxPtrLocals = 120;  // local outputs per pointer-mode encode pass
+constexpr int kBlock = 256;       // threads per workgroup (4 waves)
+constexpr int kLaneBytes = 16;    // bytes per lane per row (dwordx4)
+constexpr int kTileBytes = kBlock * kLaneBytes;
+
+// Local-parity handling inside an encode pass.
+enum LocalMode : int { kLocalNone = 0, kLocalXor = 1, kLocalZero = 2 };
+
+// Addressing of rows: either explicit pointers (one stripe; pointers live
+// in the kernel arguments) or a strided slab of `stripes` stripes.
+struct PtrRows {
+  const uint8_t* src[kMaxSrc];
+  uint8_t* dst[kMaxPassRows + kMaxPtrLocals];  // [global rows of the pass..., locals...]
+};
+
+struct SlabRows {
+  const uint8_t* base;   // slab base
+  uint64_t bstride;      // bytes between blocks of a stripe
+  uint64_t sstride;      // bytes between stripes
+};
+
+struct EncodeGeom {
+  uint64_t len;          // bytes per block
+  uint64_t tiles;        // column tiles per stripe = ceil(len / kTileBytes)
+  int stripes;
+  int k, r, groups;      // data rows, group size, local groups
+  int m;                 // total global rows (slab output indexing)
+  int row0, nrows;       // global rows of this pass [row0, row0 + nrows)
+  int local_mode;        // LocalMode
+};
+
+// Launchers return hipSuccess or the launch error.
+hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl,
+                             hipStream_t s);
+hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl,
+                              hipStream_t s);
+
+struct XorPtr {
+  const uint8_t* src[kMaxSrc];
+  uint8_t* dst;
+};
+struct XorSlab {
+  const uint8_t* base;
+  uint64_t bstride, sstride;
+  uint8_t* out;
+  uint64_t ostride;
+  int idx[kMaxSrc];      // source block indices within a stripe
+};
+struct XorGeom {
+  uint64_t len, tiles;
+  int stripes, n;
+};
+hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s);
+hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);
+
+hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes,
+                              int nblocks, uint64_t len, uint64_t seed, int s0, int b0,
+                              hipStream_t s);
+
+int device_cu_count(int device);
+
+}  // namespace ecw

@@ -1,0 +1,365 @@
+// HIP kernels for gfx950 (MI355X, CDNA4): wide-stripe GF(2^8) encode,
+// XOR reduce (CL repair / decode / relayer stage) and the synthetic fill.
+//
+// Encode replaces ECWide-C encodeData (NativeCodec.cc:137-219), which makes
+// two full passes over the k data blocks (ec_encode_data for the m global
+// rows, then one pass per local group). Here ONE pass over HBM computes all
+// global rows of a pass (<= 8) and every local XOR parity:
+//
+//   * one lane owns 16 consecutive byte columns (one dwordx4 per data row),
+//     a 256-lane workgroup a 4 KiB column tile, rows streamed with a P-deep
+//     register prefetch ring (coalesced 1 KiB per wave-instruction);
+//   * GF(2^8) products use ISA-L's 4-bit split (c*x = c*lo ^ c*(hi<<4),
+//     gf_vect_mul_init, isal:erasure_code/ec_base.c:157-262), but with the
+//     tables of ALL rows of the pass packed into one LDS entry: entry n holds
+//     byte l = c_l*n for every row l, so one ds_read per nibble serves up to
+//     4 (u32) or 8 (u64) outputs. A table record of 16 entries spans 16
+//     distinct banks: lookups are conflict-free whatever the data;
+//   * LDS addresses are formed with v_perm_b32 from a pre-masked nibble word
+//     (one v_and_or for four lookups, one v_perm per lookup); products are
+//     folded with v_bitop3_b32 (xor3);
+//   * local parities are a plain XOR of the dwordx4 rows, flushed at group
+//     boundaries (all-zero in ECWide-C literal mode, still written).
+//
+// No MFMA: the work is byte-wise GF(2^8), not a dense FP contraction.
+#include <hip/hip_runtime.h>
+
+#include <type_traits>
+
+#include "ecw_internal.hpp"
+
+namespace ecw {
+namespace {
+
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+
+__device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
+  return make_uint4(a.x ^ b.x, a.y ^ b.y, a.z ^ b.z, a.w ^ b.w);
+}
+
+typedef __attribute__((address_space(3))) const uint32_t lds_u32;
+typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
+
+// Columns are 32-bit offsets from a wave-uniform row pointer, so loads and
+// stores use the SGPR-base + VGPR-offset form (blocks are < 4 GiB; the host
+// checks it).
+template <bool TAIL>
+__device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
+  if (!TAIL || col + 16 <= len) return *reinterpret_cast<const uint4*>(row + col);
+  uint32_t w[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (col + i < len) w[i >> 2] |= static_cast<uint32_t>(row[col + i]) << (8 * (i & 3));
+  return make_uint4(w[0], w[1], w[2], w[3]);
+}
+
+template <bool TAIL>
+__device__ __forceinline__ void st16(uint8_t* row, uint32_t col, uint32_t len, uint4 v) {
+  if (!TAIL || col + 16 <= len) {
+    *reinterpret_cast<uint4*>(row + col) = v;
+    return;
+  }
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (col + i < len) row[col + i] = static_cast<uint8_t>(w[i >> 2] >> (8 * (i & 3)));
+}
+
+// ---- row addressing (all wave-uniform) -------------------------------------
+__device__ __forceinline__ const uint8_t* src_row(const PtrRows& r, const EncodeGeom&, int, int j) {
+  return r.src[j];
+}
+__device__ __forceinline__ const uint8_t* src_row(const SlabRows& r, const EncodeGeom&, int s, int j) {
+  return r.base + s * r.sstride + static_cast<uint64_t>(j) * r.bstride;
+}
+__device__ __forceinline__ uint8_t* glob_row(const PtrRows& r, const EncodeGeom&, int, int l) {
+  return r.dst[l];
+}
+__device__ __forceinline__ uint8_t* glob_row(const SlabRows& r, const EncodeGeom& g, int s, int l) {
+  return const_cast<uint8_t*>(r.base) + s * r.sstride +
+         static_cast<uint64_t>(g.k + g.row0 + l) * r.bstride;
+}
+__device__ __forceinline__ uint8_t* local_row(const PtrRows& r, const EncodeGeom& g, int, int t) {
+  return r.dst[g.nrows + t];
+}
+__device__ __forceinline__ uint8_t* local_row(const SlabRows& r, const EncodeGeom& g, int s, int t) {
+  return const_cast<uint8_t*>(r.base) + s * r.sstride +
+         static_cast<uint64_t>(g.k + g.m + t) * r.bstride;
+}
+
+// ---- GF(2^8) multiply-accumulate of one 16-byte row slice -----------------
+// acc[p] (NW=1) packs the running products of byte column p for up to 4
+// rows; NW=2: acc[2p], acc[2p+1] pack 8 rows. `rec` is the LDS byte address
+// of row j's table record (a multiple of 64*NW): its bits 8.. enter the
+// address through v_perm (jhi), its low byte through the nibble mask (jlo).
+template <int NW>
+__device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], uint32_t rec) {
+  const uint32_t jhi = rec >> 8;
+  const uint32_t jlo = (rec & 0xFFu) * 0x01010101u;
+  const uint32_t w4[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int d = 0; d < 4; ++d) {
+    const uint32_t w = w4[d];
+    // (nibble * entry size) in every byte, record low byte OR-ed in
+    const uint32_t lo = NW == 1 ? (((w << 2) & 0x3C3C3C3Cu) | jlo) : (((w << 3) & 0x78787878u) | jlo);
+    const uint32_t hi = NW == 1 ? (((w >> 2) & 0x3C3C3C3Cu) | jlo) : (((w >> 1) & 0x78787878u) | jlo);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      // address = jhi << 8 | byte b of lo/hi  (selector: S1.byte b, S0.byte0, 0, 0)
+      const uint32_t sel = 0x0C0C0400u | static_cast<uint32_t>(b);
+      const uint32_t al = __builtin_amdgcn_perm(jhi, lo, sel);
+      const uint32_t ah = __builtin_amdgcn_perm(jhi, hi, sel);
+      const int p = 4 * d + b;
+      if constexpr (NW == 1) {
+        const uint32_t tl = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(al));
+        const uint32_t th = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(ah + 64));
+        acc[p] = xor3(acc[p], tl, th);
+      } else {
+        const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al));
+        const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah + 128));
+        acc[2 * p] = xor3(acc[2 * p], static_cast<uint32_t>(tl), static_cast<uint32_t>(th));
+        acc[2 * p + 1] = xor3(acc[2 * p + 1], static_cast<uint32_t>(tl >> 32), static_cast<uint32_t>(th >> 32));
+      }
+    }
+  }
+}
+
+// byte l of the packed accumulators of columns 0..15 -> output row l
+template <int NW>
+__device__ __forceinline__ uint4 unpack_row(const uint32_t (&acc)[16 * NW], int l) {
+  const int wsel = NW == 1 ? 0 : (l >> 2);
+  const uint32_t bl = static_cast<uint32_t>(l & 3);
+  const uint32_t s01 = 0x0C0C0000u | ((4 + bl) << 8) | bl;
+  const uint32_t s23 = ((4 + bl) << 24) | (bl << 16) | 0x0C0Cu;
+  uint32_t o[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const uint32_t a0 = acc[NW * (4 * q + 0) + wsel], a1 = acc[NW * (4 * q + 1) + wsel];
+    const uint32_t a2 = acc[NW * (4 * q + 2) + wsel], a3 = acc[NW * (4 * q + 3) + wsel];
+    o[q] = __builtin_amdgcn_perm(a1, a0, s01) | __builtin_amdgcn_perm(a3, a2, s23);
+  }
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
+template <int NW, int P, int LOCAL, bool TAIL, class Rows>
+__device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& g, int s, uint32_t col,
+                                            uint32_t lds_base) {
+  const uint32_t len = static_cast<uint32_t>(g.len);
+  if (TAIL && col >= len) return;
+  const int k = g.k;
+  uint32_t acc[16 * NW];
+#pragma unroll
+  for (int i = 0; i < 16 * NW; ++i) acc[i] = 0;
+  uint4 lacc = make_uint4(0, 0, 0, 0);
+  // P-deep prefetch ring. Loads are unconditional (the index is clamped to
+  // k-1 near the end) so every ring slot is a plain load destination.
+  uint4 ring[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL>(src_row(rows, g, s, p < k ? p : k - 1), col, len);
+  int gend = g.r < k ? g.r : k;
+  int t = 0;
+  for (int j0 = 0; j0 < k; j0 += P) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      // consume slot p, then refill it with row j+P: the refill reuses the
+      // slot's registers (no copy, so no early vmcnt wait)
+      const int j = j0 + p;
+      if (j < k) {
+        gf_row<NW>(ring[p], acc, lds_base + static_cast<uint32_t>(j) * (128u * NW));
+        if constexpr (LOCAL != kLocalNone) {
+          lacc = xor4(lacc, ring[p]);
+          if (j + 1 == gend) {
+            const uint4 v = LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0);
+            st16<TAIL>(local_row(rows, g, s, t), col, len, v);
+            lacc = make_uint4(0, 0, 0, 0);
+            ++t;
+            gend = gend + g.r < k ? gend + g.r : k;
+          }
+        }
+      }
+      const int jn = j + P < k ? j + P : k - 1;
+      ring[p] = ld16<TAIL>(src_row(rows, g, s, jn), col, len);
+    }
+  }
+  for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, s, l), col, len, unpack_row<NW>(acc, l));
+}
+
+template <int NW, int P, int LOCAL, class Rows>
+__global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const EncodeGeom g,
+                                                        const uint4* __restrict__ tbl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int n16 = g.k * 8 * NW;
+  for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
+  __syncthreads();
+  // dynamic LDS starts at 0 (no static LDS in this kernel); records are
+  // 128*NW-byte aligned relative to it
+  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const int s = static_cast<int>(tile / g.tiles);
+    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+    const uint32_t col = col0 + threadIdx.x * kLaneBytes;
+    if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
+      encode_tile<NW, P, LOCAL, false>(rows, g, s, col, lds_base);
+    else
+      encode_tile<NW, P, LOCAL, true>(rows, g, s, col, lds_base);
+  }
+}
+
+// ---- XOR reduce: dst = src_0 ^ ... ^ src_{n-1} ----------------------------
+__device__ __forceinline__ const uint8_t* xsrc(const XorPtr& a, int, int i) { return a.src[i]; }
+__device__ __forceinline__ const uint8_t* xsrc(const XorSlab& a, int s, int i) {
+  return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
+}
+__device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
+__device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }
+
+template <int P, bool TAIL, class Args>
+__device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s, uint32_t col) {
+  const uint32_t len = static_cast<uint32_t>(g.len);
+  if (TAIL && col >= len) return;
+  const int n = g.n;
+  uint4 ring[P];
+#pragma unroll
+  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL>(xsrc(a, s, p < n ? p : n - 1), col, len);
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  for (int i0 = 0; i0 < n; i0 += P) {
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      const int i = i0 + p;
+      if (i < n) acc = xor4(acc, ring[p]);
+      ring[p] = ld16<TAIL>(xsrc(a, s, i + P < n ? i + P : n - 1), col, len);
+    }
+  }
+  st16<TAIL>(xdst(a, s), col, len, acc);
+}
+
+template <int P, class Args>
+__global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom g) {
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const int s = static_cast<int>(tile / g.tiles);
+    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+    const uint32_t col = col0 + threadIdx.x * kLaneBytes;
+    if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
+      xor_tile<P, false>(a, g, s, col);
+    else
+      xor_tile<P, true>(a, g, s, col);
+  }
+}
+
+// ---- synthetic fill (ecwide.h: ecw_fill_random_dev) ------------------------
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+  z ^= z >> 30;
+  z *= 0xBF58476D1CE4E5B9ull;
+  z ^= z >> 27;
+  z *= 0x94D049BB133111EBull;
+  z ^= z >> 31;
+  return z;
+}
+
+__global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bstride, uint64_t sstride,
+                                                      int stripes, int nblocks, uint64_t len,
+                                                      uint64_t seed, int s0, int b0) {
+  constexpr uint64_t G = 0x9E3779B97F4A7C15ull;
+  const uint64_t nw = (len + 7) / 8;
+  const uint64_t npair = (nw + 1) / 2;
+  for (int y = blockIdx.y; y < stripes * nblocks; y += gridDim.y) {
+    const int s = y / nblocks, b = y - s * nblocks;
+    const uint64_t key = mix64(seed + G * (1ull + static_cast<uint64_t>(s0 + s) * 65536ull +
+                                           static_cast<uint64_t>(b0 + b)));
+    uint8_t* p = dst + s * sstride + static_cast<uint64_t>(b) * bstride;
+    for (uint64_t q = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; q < npair;
+         q += static_cast<uint64_t>(gridDim.x) * kBlock) {
+      const uint64_t w0 = 2 * q;
+      const uint64_t v0 = mix64(key + w0 * G), v1 = mix64(key + (w0 + 1) * G);
+      const uint64_t off = 8 * w0;
+      if (off + 16 <= len) {
+        *reinterpret_cast<uint4*>(p + off) = make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(v0 >> 32),
+                                                        static_cast<uint32_t>(v1), static_cast<uint32_t>(v1 >> 32));
+      } else {
+        for (int i = 0; i < 16 && off + i < len; ++i)
+          p[off + i] = static_cast<uint8_t>((i < 8 ? v0 >> (8 * i) : v1 >> (8 * (i - 8))));
+      }
+    }
+  }
+}
+
+constexpr int kPrefetchEnc = 4;
+constexpr int kPrefetchXor = 8;
+
+unsigned grid_for(uint64_t tiles_total) {
+  // memory-bound streaming: enough workgroups to fill 256 CUs several deep,
+  // grid-stride for the rest (tables are staged once per workgroup)
+  const uint64_t cap = 256ull * 8ull;
+  return static_cast<unsigned>(tiles_total < cap ? (tiles_total ? tiles_total : 1) : cap);
+}
+
+template <int NW, class Rows>
+hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
+  switch (g.local_mode) {
+    case kLocalXor:
+      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    case kLocalZero:
+      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalZero, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    default:
+      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+  }
+  return hipGetLastError();
+}
+
+template <class Rows>
+hipError_t launch_encode(const Rows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s) {
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  if (total == 0) return hipSuccess;
+  if (g.nrows < 1 || g.nrows > kMaxPassRows || g.k < 1 || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  const dim3 grid(grid_for(total));
+  const uint4* tbl = static_cast<const uint4*>(d_tbl);
+  return g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
+}
+
+template <class Args>
+hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  if (total == 0) return hipSuccess;
+  if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), dim3(grid_for(total)), dim3(kBlock), 0, s, a, g);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s) {
+  return launch_encode(rows, g, d_tbl, s);
+}
+hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl, hipStream_t s) {
+  return launch_encode(slab, g, d_tbl, s);
+}
+hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
+hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
+
+hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes, int nblocks,
+                              uint64_t len, uint64_t seed, int s0, int b0, hipStream_t s) {
+  if (stripes <= 0 || nblocks <= 0 || len == 0) return hipSuccess;
+  const uint64_t npair = ((len + 7) / 8 + 1) / 2;
+  uint64_t gx = (npair + kBlock - 1) / kBlock;
+  if (gx > 1024) gx = 1024;
+  const int rows = stripes * nblocks;
+  const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(rows < 65535 ? rows : 65535));
+  hipLaunchKernelGGL(fill_kernel, grid, dim3(kBlock), 0, s, dst, bstride, sstride, stripes, nblocks, len,
+                     seed, s0, b0);
+  return hipGetLastError();
+}
+
+int device_cu_count(int device) {
+  int n = 0;
+  if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return 0;
+  return n;
+}
+
+}  // namespace ecw
