@@ -47,9 +47,9 @@ def parse():
 def dist_setup(args):
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    from ecwide_amd.shard import dist_env
+
+    world, rank, local = dist_env()
     if world > 1:
         import torch.distributed as dist
 
@@ -107,9 +107,11 @@ def cpu_baseline(args, k, m, r):
         # decodeData: ec_encode_data with the all-ones table (NativeCodec.cc:248)
         return orc.encode_data(ones, data[1:r] + [par[m]], 1, avx2=True)[0]
 
+    from ecwide_amd.shard import host_threads
+
+    t1 = host_threads()
     res = {}
-    for threads in (1, os.cpu_count() or 1):
-        threads = min(threads, 64)
+    for threads in sorted({1, t1}):
         run(threads)  # warm
         n, t0 = 0, time.perf_counter()
         while True:
@@ -120,7 +122,6 @@ def cpu_baseline(args, k, m, r):
                 break
         assert np.array_equal(rep, data[0])
         res[threads] = n * per_stripe / el / 1e9
-    t1 = min(os.cpu_count() or 1, 64)
     return {
         "value": round(res[1], 3),
         "unit": "GB/s",
@@ -150,7 +151,10 @@ def main():
     S = args.stripes
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
-    slab.fill_random(seed=args.seed, s0=rank * S)
+    from ecwide_amd.shard import weak_shard
+
+    s0, _ = weak_shard(S, rank)  # each rank owns distinct stripe ids, no data exchange
+    slab.fill_random(seed=args.seed, s0=s0)
     torch.cuda.synchronize()
     enc_bytes = slab.encode_bytes()
     rep_bytes = slab.repair_bytes(0)

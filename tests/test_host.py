@@ -1,0 +1,143 @@
+"""CPU tests of the product's host side through the C ABI: the library
+loads, exports everything include/ecwide.h declares, and computes the
+reference's geometry, matrices and tables. No kernel launches here."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+
+import ecwide_amd as E
+from ecwide_amd import _lib
+
+# ECWide-C/config/scheme.ini (the reference's default scheme, verbatim data)
+DEFAULT_INI = "codeType = CL\nk = 32\ngroupDataNum = 11\nglobalParityNum = 3\nchunkSizeBits = 26"
+
+
+def test_exports_every_header_symbol():
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    syms = _lib.header_symbols()
+    assert len(syms) >= 25
+    for s in syms:
+        assert hasattr(lib, s), s
+    assert set(syms) == set(_lib.SIGNATURES), "ctypes signatures out of sync with the header"
+    assert _lib.lib.ecw_abi_version() == 1
+
+
+def test_library_is_hip_code_for_gfx950():
+    data = open(_lib.LIB_PATH, "rb").read()
+    assert b"gfx950" in data  # offload bundle for MI355X
+    assert b"encode_kernel" in data and b"xor_kernel" in data
+
+
+def test_default_scheme_ini(tmp_path):
+    p = tmp_path / "scheme.ini"
+    p.write_text(DEFAULT_INI)
+    s = E.CodingScheme.getFromConfig(str(p))
+    assert (s.codeType, s.k, s.groupDataNum, s.m, s.chunkSize) == ("CL", 32, 11, 3, 1 << 26)
+    assert (s.groupNum, s.rackNodesNum, s.rackNum, s.chunkSizeBits) == (3, 4, 10, 26)
+
+
+@pytest.mark.parametrize("text,code,fields", [
+    ("codeType = LRC\nk = 12\ngroupDataNum = 4\nglobalParityNum = 2\nchunkSizeBits = 12\n", "LRC", (12, 2, 4, 3, -1, -1)),
+    ("codeType = TL\nk = 12\nglobalParityNum = 3\nchunkSizeBits = 10", "TL", (12, 3, -1, 0, 3, 5)),
+    ("codeType = RS\nk = 6\nglobalParityNum = 3\nchunkSizeBits = 4\n\n", "RS", (6, 3, -1, 0, 0, 0)),
+    ("k = 128\nglobalParityNum = 3\ngroupDataNum = 27\nchunkSizeBits = 26", "CL", (128, 3, 27, 5, 4, 35)),
+])
+def test_ini_code_types(text, code, fields):
+    s = E.CodingScheme.fromConfigText(text)
+    assert s.codeType == code
+    assert (s.k, s.m, s.groupDataNum, s.groupNum, s.rackNodesNum, s.rackNum) == fields
+
+
+@pytest.mark.parametrize("text", ["k = 32\nglobalParityNum = 3\nchunkSizeBits = 26",  # CL without r
+                                  "codeType = CL\nk = x\ngroupDataNum = 11\nglobalParityNum = 3\nchunkSizeBits = 26",
+                                  "codeType = CL\nk 32\n", "codeType = RS\nk = 300\nglobalParityNum = 3\nchunkSizeBits = 4"])
+def test_ini_errors(text):
+    with pytest.raises(E.EcwError):
+        E.CodingScheme.fromConfigText(text)
+
+
+def test_ini_missing_file():
+    with pytest.raises(E.EcwError) as ei:
+        E.CodingScheme.getFromConfig("/nonexistent/scheme.ini")
+    assert ei.value.status == -7
+
+
+CODECS = [("C", 32, 3, 11), ("C", 32, 2, 8), ("C", 128, 3, 27), ("C", 10, 4, 3), ("C", 64, 3, 11), ("C", 64, 3, 7),
+          ("C", 5, 1, 5), ("L", 12, 2, 4), ("L", 16, 2, 4), ("T", 12, 3, -1), ("T", 13, 4, -1), ("R", 12, 4, -1)]
+
+
+def _nodes(t, k, m, r):
+    if t == "C":
+        g = -(-k // r)
+        return range(1, k + g + m + 1)
+    return range(1, k + m + 1)
+
+
+@pytest.mark.parametrize("t,k,m,r", CODECS)
+def test_codec_geometry_matches_oracle(orc, t, k, m, r):
+    code = {"C": "CL", "L": "LRC", "T": "TL", "R": "RS"}[t]
+    s = E.CodingScheme._make(code, k, m, r, 4096)
+    for node in _nodes(t, k, m, r):
+        c = E.NativeCodec(s, node, False)
+        o = orc.codec(t, k, m, r, 4096, node)
+        assert (c.encodeDataNum, c.decodeDataNum, c.partialDecodeNum) == (
+            o.encode_data_num, o.decode_data_num, o.partial_decode_num), node
+        assert c.groupNum == o.group_num and c.parityNum == o.parity_num
+        if t == "C":
+            assert c.rackPerGroup == o.rack_per_group
+    c = E.NativeCodec(s, 1, False)
+    o = orc.codec(t, k, m, r, 4096, 1)
+    assert np.array_equal(c.getEncodeMatrix(), o.encode_matrix())
+    assert np.array_equal(c.getEncodeGftbl(), o.encode_gftbl())
+    ones = orc.init_tables(c.decodeDataNum, 1, np.ones(c.decodeDataNum, np.uint8))
+    assert np.array_equal(c.getDecodeGftbl(), ones)
+
+
+def test_matrices_vs_golden(manifest):
+    for key, hexv in manifest["matrices"].items():
+        kind, a, b = key.split("_")
+        if kind != "cauchy":
+            continue
+        c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(int(a), int(b), 64))
+        assert c.getEncodeMatrix().tobytes().hex() == hexv, key
+
+
+def test_paper_stripe_geometry():
+    """(n,k,r,z) = (136,128,27,34) CL: 5 groups, 34+1 racks of 4 (paper p.238)."""
+    s = E.CodingScheme.getClScheme(128, 3, 27, 1 << 26)
+    c = E.NativeCodec.getClCodec(s, 1, False)
+    assert (s.groupNum, s.rackNodesNum, s.rackNum) == (5, 4, 35)
+    assert (c.decodeDataNum, c.partialDecodeNum, c.rackPerGroup) == (9, 4, 7)
+    assert c.repairSources(0) == list(range(1, 27)) + [131]
+    assert c.repairSources(135) == list(range(108, 128))  # last local parity: its 20 data blocks
+    assert c.repairSources(127) == list(range(108, 127)) + [135]
+
+
+def test_errors():
+    s = E.CodingScheme.getClScheme(8, 2, 4, 64)
+    with pytest.raises(E.EcwError):
+        E.NativeCodec(s, 0, False)  # node indices are 1-based
+    with pytest.raises(E.EcwError):
+        E.CodingScheme.getClScheme(250, 7, 10, 64)  # k + m > 256
+    with pytest.raises(E.EcwError):
+        E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(4, 2, 64)).repairSources(0)  # no local groups
+    c = E.NativeCodec(s, 1, True)  # multi-node geometry: counts only
+    assert c.encodeDataNum == 4
+    with pytest.raises(E.EcwError) as ei:
+        c.encodeData([np.zeros(64, np.uint8)] * 4, [np.zeros(64, np.uint8)] * 4)
+    assert ei.value.status == -5
+
+
+@pytest.mark.skipif(E.device_count() > 0, reason="checks the no-GPU failure mode")
+def test_device_calls_fail_loudly_without_gpu():
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(4, 2, 2, 64), 1, False)
+    with pytest.raises(E.EcwError) as ei:
+        c.encodeData([np.zeros(64, np.uint8)] * 4, [np.zeros(64, np.uint8)] * 4)
+    assert ei.value.status == -3
+
+
+def test_status_strings():
+    for st in range(0, -8, -1):
+        assert _lib.lib.ecw_status_string(st)
