@@ -12,7 +12,10 @@ namespace ecw {
 constexpr int kMaxSrc = 256;      // k + m <= 256 for a GF(2^8) Cauchy code
 constexpr int kMaxPassRows = 8;   // global rows per encode pass (u64 packed entries)
 constexpr int kMaxPtrLocals = 120;  // local outputs per pointer-mode encode pass
-constexpr int kBlock = 256;       // threads per workgroup (4 waves)
+#ifndef ECW_BLOCK
+#define ECW_BLOCK 256
+#endif
+constexpr int kBlock = ECW_BLOCK; // threads per workgroup
 constexpr int kLaneBytes = 16;    // bytes per lane per row (dwordx4)
 constexpr int kTileBytes = kBlock * kLaneBytes;
 

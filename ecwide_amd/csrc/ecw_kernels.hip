@@ -45,9 +45,27 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 // Columns are 32-bit offsets from a wave-uniform row pointer, so loads and
 // stores use the SGPR-base + VGPR-offset form (blocks are < 4 GiB; the host
 // checks it).
+#ifndef ECW_NT_LOADS
+#define ECW_NT_LOADS 0
+#endif
+#ifndef ECW_ABLATE
+#define ECW_ABLATE 0  // tuning builds only: 1 = skip the GF lookups, 2 = skip the data loads
+#endif
+
 template <bool TAIL>
 __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
+#if ECW_ABLATE == 2
+  if (!TAIL) return make_uint4(col ^ static_cast<uint32_t>(reinterpret_cast<uintptr_t>(row)), col * 3u, col + 7u, col >> 3);
+#endif
+#if ECW_NT_LOADS
+  if (!TAIL || col + 16 <= len) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + col));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+#else
   if (!TAIL || col + 16 <= len) return *reinterpret_cast<const uint4*>(row + col);
+#endif
   uint32_t w[4] = {0, 0, 0, 0};
 #pragma unroll
   for (int i = 0; i < 16; ++i)
@@ -167,7 +185,12 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
       // slot's registers (no copy, so no early vmcnt wait)
       const int j = j0 + p;
       if (j < k) {
+#if ECW_ABLATE == 1
+        acc[0] ^= ring[p].x;
+        acc[1] ^= ring[p].y;
+#else
         gf_row<NW>(ring[p], acc, lds_base + static_cast<uint32_t>(j) * (128u * NW));
+#endif
         if constexpr (LOCAL != kLocalNone) {
           lacc = xor4(lacc, ring[p]);
           if (j + 1 == gend) {
@@ -287,13 +310,23 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
   }
 }
 
-constexpr int kPrefetchEnc = 4;
-constexpr int kPrefetchXor = 8;
+// Tunables (overridable with -D for tuning builds; tools/variants.py)
+#ifndef ECW_PREFETCH_ENC
+#define ECW_PREFETCH_ENC 2
+#endif
+#ifndef ECW_PREFETCH_XOR
+#define ECW_PREFETCH_XOR 8
+#endif
+#ifndef ECW_GRID_PER_CU
+#define ECW_GRID_PER_CU 64
+#endif
+constexpr int kPrefetchEnc = ECW_PREFETCH_ENC;
+constexpr int kPrefetchXor = ECW_PREFETCH_XOR;
 
 unsigned grid_for(uint64_t tiles_total) {
   // memory-bound streaming: enough workgroups to fill 256 CUs several deep,
   // grid-stride for the rest (tables are staged once per workgroup)
-  const uint64_t cap = 256ull * 8ull;
+  const uint64_t cap = 256ull * ECW_GRID_PER_CU;
   return static_cast<unsigned>(tiles_total < cap ? (tiles_total ? tiles_total : 1) : cap);
 }
 

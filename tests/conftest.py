@@ -16,11 +16,12 @@ def pytest_configure(config):
 
 
 def pytest_collection_modifyitems(config, items):
-    import torch
-
-    if torch.cuda.is_available():
+    # Skip GPU tests only where there is no GPU device node at all (the CPU
+    # container). On a GPU box a runtime that cannot see the GPU must FAIL the
+    # tests (their fixtures assert), never silently skip them.
+    if os.path.exists("/dev/kfd"):
         return
-    skip = pytest.mark.skip(reason="no GPU in this container")
+    skip = pytest.mark.skip(reason="no GPU device (/dev/kfd) on this host")
     for it in items:
         if "gpu" in it.keywords:
             it.add_marker(skip)

@@ -1,0 +1,91 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of libecwide.so variants on one GPU (one process,
+same data, rounds interleaved: cdna_hip_programming.md §5.4 rule 24).
+
+  python tools/kbench.py [--k 128 --m 3 --r 27 --mib 64 --stripes 4 --rounds 5] build/variants/*.so
+"""
+import argparse
+import ctypes
+import os
+import statistics
+import sys
+from ctypes import byref, c_void_p
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("libs", nargs="+")
+    ap.add_argument("--k", type=int, default=128)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--r", type=int, default=27)
+    ap.add_argument("--mib", type=float, default=64)
+    ap.add_argument("--stripes", type=int, default=4)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--check", action="store_true")
+    ap.add_argument("--code", default="C", help="C (CL, locals) or R (RS, globals only)")
+    a = ap.parse_args()
+    import torch
+
+    from ecwide_amd import _lib
+
+    k, m, r = a.k, a.m, a.r
+    B = int(a.mib * (1 << 20))
+    g = -(-k // r) if a.code == "C" else 0
+    nblk = k + m + g
+    bstride = (B + 4096 + 255) // 256 * 256
+    sstride = nblk * bstride
+    S = a.stripes
+    buf = torch.empty(S * sstride, dtype=torch.uint8, device="cuda")
+    out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
+    stream = c_void_p(torch.cuda.current_stream().cuda_stream)
+    libs = []
+    for path in a.libs:
+        L = _lib.load(path)
+        sch = _lib.ecw_scheme()
+        assert L.ecw_scheme_init(byref(sch), a.code.encode(), k, m, r, B) == 0
+        h = c_void_p()
+        assert L.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(h)) == 0
+        libs.append((os.path.basename(path), L, h))
+    L0 = libs[0][1]
+    assert L0.ecw_fill_random_dev(0, c_void_p(buf.data_ptr()), bstride, sstride, S, k, B, 1, 0, 0, stream) == 0
+    enc_bytes = S * nblk * B
+    rep_bytes = S * (r + 1) * B
+    ref = None
+    if a.check:
+        assert libs[0][1].ecw_encode_batch_dev(libs[0][2], c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream) == 0
+        torch.cuda.synchronize()
+        ref = buf[(k) * bstride:(k) * bstride + B].clone()
+    res = {n: ([], []) for n, _, _ in libs}
+    for rd in range(a.rounds):
+        for name, L, h in libs:
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            for it in range(a.iters + 1):
+                if it == 1:
+                    e[0].record()
+                st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
+                assert st == 0, (name, st)
+            e[1].record()
+            for it in range(a.iters if a.code == "C" else 0):
+                st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
+                                            c_void_p(out.data_ptr()), B, B, stream)
+                assert st == 0, (name, st)
+            e[2].record()
+            torch.cuda.synchronize()
+            res[name][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
+            res[name][1].append(rep_bytes * a.iters / max(e[1].elapsed_time(e[2]), 1e-6) / 1e3 / 1e9 * 1e3)
+            if ref is not None and "ablate" not in name:
+                got = buf[(k) * bstride:(k) * bstride + B]
+                if not torch.equal(got, ref):
+                    print(f"  !! {name}: parity differs from {libs[0][0]}")
+    print(f"CL(k={k},r={r},m={m}) B={a.mib} MiB x{S} stripes; GB/s median (min..max) over {a.rounds} rounds")
+    for name, (en, rp) in res.items():
+        print(f"{name:28s} encode {statistics.median(en):8.1f} ({min(en):7.1f}..{max(en):7.1f})   "
+              f"repair {statistics.median(rp):8.1f} ({min(rp):7.1f}..{max(rp):7.1f})", flush=True)
+
+
+if __name__ == "__main__":
+    main()
