@@ -72,6 +72,7 @@ SIGNATURES = {
     "ecw_decode": (c_int, [c_void_p, _pp, c_void_p, c_size_t]),
     "ecw_partial_decode": (c_int, [c_void_p, _pp, c_void_p, c_size_t]),
     "ecw_xor_intermediate": (c_int, [c_void_p, _pp, _pp, c_size_t]),
+    "ecw_repair": (c_int, [c_void_p, _pp, c_int, c_void_p, c_size_t]),
     "ecw_encode_dev": (c_int, [c_void_p, _pp, _pp, c_size_t, c_void_p]),
     "ecw_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
     "ecw_partial_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
@@ -93,7 +94,20 @@ def header_symbols(path: str = HEADER) -> list:
     return sorted(set(re.findall(r"\b(ecw_[a-z0-9_]+)\s*\(", text)) - {"ecw_status"})
 
 
+def _torch_runtime_first() -> None:
+    """torch bundles its own libamdhip64.so.7 (same SONAME as /opt/rocm's).
+    Whichever is loaded first serves the whole process, and torch does not
+    see the GPU when it finds a different runtime already loaded. So when
+    torch is installed it is imported first and libecwide.so binds to the
+    runtime torch brought; C/C++ callers simply get /opt/rocm's."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    _torch_runtime_first()
     if not os.path.exists(path):
         raise ImportError(
             f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "

@@ -250,6 +250,16 @@ class NativeCodec:
         else:
             _check(lib.ecw_xor_intermediate(self._h, _parr(source), _parr(target), n), "xorIntemediate")
 
+    def repairBlock(self, blocks, lost_block: int, out, length=None) -> None:
+        """Flat CL repair of one block from a stripe's blocks ([D.., G.., L..]
+        order; the lost entry may be None). Host buffers only."""
+        srcs = self.repairSources(lost_block)
+        n = length if length is not None else min(_nbytes(blocks[i]) for i in srcs)
+        arr = (c_void_p * len(blocks))()
+        for i, b in enumerate(blocks):
+            arr[i] = _addr(b) if b is not None else None
+        _check(lib.ecw_repair(self._h, arr, lost_block, _addr(out), n), "repairBlock")
+
     # -- CL repair fan-in (ClMetadataManager.java:137-257, flattened) --------
     def repairSources(self, lost_block: int) -> list:
         buf = (c_int * 256)()

@@ -65,6 +65,7 @@ struct ecw_codec {
   bool xori_called = false;           // per-codec replacement of the static `flag`
   // staging for the host-memory entry points
   hipStream_t stream = nullptr;
+  struct HostPipe* pipe = nullptr;    // streams/events of the host-memory pipeline
   uint8_t* d_stage = nullptr;
   size_t stage_bytes = 0;
 
@@ -74,8 +75,10 @@ struct ecw_codec {
       for (void* p : d_pass) (void)hipFree(p);
       if (d_stage) (void)hipFree(d_stage);
       if (stream) (void)hipStreamDestroy(stream);
+      destroy_pipe();
     }
   }
+  void destroy_pipe();
 
   bool has_local() const { return info.code_type == 'C' || info.code_type == 'L'; }
   int k() const { return info.encode_data_num; }
@@ -568,11 +571,43 @@ int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t 
 }
 
 // ---- host-memory entry points (blocking) ------------------------------------
-// Inputs are copied into a per-codec HBM staging area, the kernels run, the
-// outputs come back. Serialised per codec (the staging area is shared).
+// The blocks stay in host memory (files / Java direct ByteBuffers in the
+// reference). Columns are independent, so the call is pipelined over column
+// slices of kHostChunk bytes through kSlots HBM staging slots on three
+// streams: H2D copies of slice i+1 overlap the kernel on slice i and the D2H
+// copies of slice i-1. With pinned (hipHostMalloc / registered) buffers the
+// copies are DMA at PCIe rate; pageable buffers work too (HIP stages them).
+// Serialised per codec (the staging slots are per codec).
+constexpr size_t kHostChunk = size_t(8) << 20;
+constexpr int kSlots = 3;
+
+struct HostPipe {
+  hipStream_t s_in = nullptr, s_run = nullptr, s_out = nullptr;
+  hipEvent_t ev_in[kSlots] = {}, ev_run[kSlots] = {}, ev_out[kSlots] = {};
+  bool ok = false;
+  int init() {
+    if (ok) return ECW_OK;
+    for (hipStream_t* st : {&s_in, &s_run, &s_out})
+      if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) return ECW_EDEVICE;
+    for (int i = 0; i < kSlots; ++i)
+      for (hipEvent_t* e : {&ev_in[i], &ev_run[i], &ev_out[i]})
+        if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return ECW_EDEVICE;
+    ok = true;
+    return ECW_OK;
+  }
+  void destroy() {
+    for (hipStream_t st : {s_in, s_run, s_out})
+      if (st) (void)hipStreamDestroy(st);
+    for (int i = 0; i < kSlots; ++i)
+      for (hipEvent_t e : {ev_in[i], ev_run[i], ev_out[i]})
+        if (e) (void)hipEventDestroy(e);
+  }
+};
+
+typedef int (*host_op)(ecw_codec*, uint8_t* const*, int, uint8_t* const*, int, size_t, hipStream_t);
+
 static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8_t* const* out, int nout,
-                          size_t len, int (*op)(ecw_codec*, uint8_t* const*, int, uint8_t* const*, int, size_t,
-                                                hipStream_t)) {
+                          size_t len, host_op op) {
   for (int i = 0; i < nin; ++i)
     if (!in[i]) return ECW_EINVAL;
   for (int i = 0; i < nout; ++i)
@@ -583,19 +618,52 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
-  const size_t stride = (len + 255) & ~static_cast<size_t>(255);
-  st = c->ensure_stage(stride * (nin + nout));
-  if (st) return st;
+  if (!c->pipe) {
+    c->pipe = new (std::nothrow) HostPipe();
+    if (!c->pipe) return ECW_ENOMEM;
+  }
+  HostPipe& P = *c->pipe;
+  if ((st = P.init())) return st;
+  const size_t chunk = std::min(len, kHostChunk);
+  const size_t cstride = (chunk + 255) & ~static_cast<size_t>(255);
+  const size_t slot_bytes = cstride * (nin + nout);
+  if ((st = c->ensure_stage(slot_bytes * kSlots))) return st;
   std::vector<uint8_t*> din(nin), dout(nout);
-  for (int i = 0; i < nin; ++i) din[i] = c->d_stage + i * stride;
-  for (int i = 0; i < nout; ++i) dout[i] = c->d_stage + (nin + i) * stride;
-  for (int i = 0; i < nin; ++i)
-    if (hipMemcpyAsync(din[i], in[i], len, hipMemcpyHostToDevice, c->stream) != hipSuccess) return ECW_EDEVICE;
-  st = op(c, din.data(), nin, dout.data(), nout, len, c->stream);
-  if (st) return st;
-  for (int i = 0; i < nout; ++i)
-    if (hipMemcpyAsync(out[i], dout[i], len, hipMemcpyDeviceToHost, c->stream) != hipSuccess) return ECW_EDEVICE;
-  return hipStreamSynchronize(c->stream) == hipSuccess ? ECW_OK : ECW_EDEVICE;
+  size_t i = 0;
+  for (size_t c0 = 0; c0 < len; c0 += chunk, ++i) {
+    const int slot = static_cast<int>(i % kSlots);
+    const size_t n = std::min(chunk, len - c0);
+    uint8_t* base = c->d_stage + slot * slot_bytes;
+    for (int b = 0; b < nin; ++b) din[b] = base + b * cstride;
+    for (int b = 0; b < nout; ++b) dout[b] = base + (nin + b) * cstride;
+    if (i >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return ECW_EDEVICE;
+    for (int b = 0; b < nin; ++b)
+      if (hipMemcpyAsync(din[b], in[b] + c0, n, hipMemcpyHostToDevice, P.s_in) != hipSuccess) return ECW_EDEVICE;
+    if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return ECW_EDEVICE;
+    if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return ECW_EDEVICE;
+    if ((st = op(c, din.data(), nin, dout.data(), nout, n, P.s_run))) return st;
+    if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return ECW_EDEVICE;
+    if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return ECW_EDEVICE;
+    for (int b = 0; b < nout; ++b)
+      if (hipMemcpyAsync(out[b] + c0, dout[b], n, hipMemcpyDeviceToHost, P.s_out) != hipSuccess) return ECW_EDEVICE;
+    if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return ECW_EDEVICE;
+  }
+  if (hipStreamSynchronize(P.s_out) != hipSuccess) return ECW_EDEVICE;
+  return hipStreamSynchronize(P.s_run) == hipSuccess ? ECW_OK : ECW_EDEVICE;
+}
+
+void ecw_codec::destroy_pipe() {
+  if (pipe) {
+    pipe->destroy();
+    delete pipe;
+    pipe = nullptr;
+  }
+}
+
+static int op_zero(ecw_codec*, uint8_t* const*, int, uint8_t* const* dout, int nout, size_t len, hipStream_t s) {
+  for (int b = 0; b < nout; ++b)
+    if (hipMemsetAsync(dout[b], 0, len, s) != hipSuccess) return ECW_EDEVICE;
+  return ECW_OK;
 }
 
 static int op_encode(ecw_codec* c, uint8_t* const* din, int, uint8_t* const* dout, int, size_t len, hipStream_t s) {
@@ -627,6 +695,19 @@ int ecw_partial_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target
   return host_roundtrip(c, data, c->info.partial_decode_num, out, 1, len, op_xor);
 }
 
+int ecw_repair(ecw_codec* c, const uint8_t* const* blocks, int lost, uint8_t* out, size_t len) {
+  if (!c || !blocks || !out || !check_len(len)) return ECW_EINVAL;
+  if (c->info.local_mode == ECW_LOCAL_LITERAL) return ECW_EUNSUPPORTED;  // literal L blocks are zeros
+  int idx[kMaxSrc];
+  const int n = ecw_repair_sources(c, lost, idx, kMaxSrc);
+  if (n < 0) return n;
+  if (n == 0) return ECW_EUNSUPPORTED;
+  std::vector<const uint8_t*> src(n);
+  for (int i = 0; i < n; ++i) src[i] = blocks[idx[i]];
+  uint8_t* const o[1] = {out};
+  return host_roundtrip(c, src.data(), n, o, 1, len, op_xor);
+}
+
 int ecw_xor_intermediate(ecw_codec* c, const uint8_t* const* source, uint8_t* const* target, size_t len) {
   if (!c || !source || !target || !check_len(len)) return ECW_EINVAL;
   const int m = c->m();
@@ -638,8 +719,11 @@ int ecw_xor_intermediate(ecw_codec* c, const uint8_t* const* source, uint8_t* co
   }
   for (int i = 0; i < m; ++i) {
     if (!source[i] || !target[i]) return ECW_EINVAL;
-    if (zero_first) {
-      std::memset(target[i], 0, len);  // the reference's first-call output (NativeCodec.cc:287-292)
+    if (zero_first) {  // the reference's first-call output (NativeCodec.cc:287-292), made on the device
+      const uint8_t* in1[1] = {source[i]};
+      uint8_t* const out1[1] = {target[i]};
+      const int st = host_roundtrip(c, in1, 0, out1, 1, len, op_zero);
+      if (st) return st;
       continue;
     }
     const uint8_t* in[2] = {source[i], target[i]};

@@ -26,7 +26,8 @@
  *   ecw_*_dev                 the same operations on HBM-resident blocks (stream-ordered)
  *   ecw_encode_batch_dev /    batches of independent stripes in one launch (north_star:
  *   ecw_repair_batch_dev      "stripes are independent by byte range")
- *   ecw_repair_sources        the flat fan-in of a CL single-block repair,
+ *   ecw_repair / ecw_repair_sources
+ *                             the flat fan-in of a CL single-block repair,
  *                             ClMetadataManager.getChunkRepairTask  ECWide-C/src/ClMetadataManager.java:137-257
  *
  * Conventions (mirroring the reference):
@@ -168,6 +169,11 @@ int ecw_partial_decode(ecw_codec* codec, const uint8_t* const* data, uint8_t* ta
                        size_t len);
 int ecw_xor_intermediate(ecw_codec* codec, const uint8_t* const* source, uint8_t* const* target,
                          size_t len);
+
+/* Flat CL single-block repair on host memory: `blocks` holds every block of
+ * one stripe in slab order [D.., G.., L..] (the lost one may be NULL);
+ * `out` receives the rebuilt `lost_block` (D or L). */
+int ecw_repair(ecw_codec* codec, const uint8_t* const* blocks, int lost_block, uint8_t* out, size_t len);
 
 /* ---- device-memory entry points (asynchronous on `stream`) -------------
  * All pointers are HBM addresses, 16-byte aligned. The pointer arrays

@@ -190,6 +190,30 @@ def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S):
             assert torch.equal(out[st * o:st * o + B], slab.block(st, lost)), (lost, st)
 
 
+@pytest.mark.parametrize("B", [(20 << 20) + 37, (8 << 20), 4096 * 3 + 5])
+def test_host_pipeline_multi_chunk_and_repair(E, torch, orc, B):
+    """ecw_encode / ecw_repair on host buffers larger than one 8 MiB pipeline
+    slice (ragged tail), pageable and pinned, vs the oracle."""
+    k, m, r = 10, 2, 4
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    data = [orc.fill(B, 77, 0, j) for j in range(k)]
+    want = orc.codec("C", k, m, r, B).encode(data, threads=8)
+    par = [np.zeros(B, np.uint8) for _ in range(c.parityNum)]
+    c.encodeData(data, par)
+    for i, (g, w) in enumerate(zip(par, want)):
+        assert np.array_equal(g, w), i
+    pinned = [torch.empty(B, dtype=torch.uint8, pin_memory=True).numpy() for _ in range(k + c.parityNum)]
+    for j in range(k):
+        pinned[j][:] = data[j]
+    c.encodeData(pinned[:k], pinned[k:])
+    assert all(np.array_equal(a, b) for a, b in zip(pinned[k:], want))
+    blocks = data + par
+    for lost in (0, k - 1, k + m):
+        out = np.zeros(B, np.uint8)
+        c.repairBlock([b if i != lost else None for i, b in enumerate(blocks)], lost, out)
+        assert np.array_equal(out, blocks[lost]), lost
+
+
 def test_literal_mode_slab_writes_zero_locals(E, torch):
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(32, 2, 8, 65536), 1, False, local_mode="literal")
     slab = E.StripeSlab(c, stripes=2, block_bytes=65536)

@@ -14,3 +14,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_fetch_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc1.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_write_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc2.log 2>&1 || exit $?
 echo "profiles done"
+#cd $GRAFT_REPO_ROOT && timeout -k 10 400 python bench.py --host-resident --steps 12 > gpurun_out/bench_host.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_host.log

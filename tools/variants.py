@@ -13,7 +13,11 @@ from concurrent.futures import ThreadPoolExecutor
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
-from ecwide_amd import build as b  # noqa: E402
+import importlib.util  # noqa: E402
+
+_spec = importlib.util.spec_from_file_location("ecw_build", os.path.join(REPO, "ecwide_amd", "build.py"))
+b = importlib.util.module_from_spec(_spec)
+_spec.loader.exec_module(b)
 
 OUT = os.path.join(REPO, "build", "variants")
 
