@@ -73,6 +73,8 @@ SIGNATURES = {
     "ecw_partial_decode": (c_int, [c_void_p, _pp, c_void_p, c_size_t]),
     "ecw_xor_intermediate": (c_int, [c_void_p, _pp, _pp, c_size_t]),
     "ecw_repair": (c_int, [c_void_p, _pp, c_int, c_void_p, c_size_t]),
+    "ecw_encode_stripes": (c_int, [c_void_p, c_int, _pp, _pp, c_size_t]),
+    "ecw_matrix_codec_create": (c_int, [_u8p, c_int, c_int, c_int, POINTER(c_void_p)]),
     "ecw_encode_dev": (c_int, [c_void_p, _pp, _pp, c_size_t, c_void_p]),
     "ecw_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
     "ecw_partial_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),

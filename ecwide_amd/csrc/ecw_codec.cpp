@@ -398,6 +398,35 @@ int ecw_codec_create(const ecw_scheme* sch, int node_index, int multinode, int l
 
 void ecw_codec_destroy(ecw_codec* codec) { delete codec; }
 
+int ecw_matrix_codec_create(const uint8_t* matrix, int k, int rows, int device, ecw_codec** out) {
+  if (!matrix || !out || k < 1 || rows < 1 || k > kMaxSrc || rows > 255) return ECW_EINVAL;
+  *out = nullptr;
+  ecw_codec* c = new (std::nothrow) ecw_codec();
+  if (!c) return ECW_ENOMEM;
+  c->device = device;
+  c->scheme.code_type = 'M';
+  c->scheme.k = k;
+  c->scheme.global_parity_num = rows;
+  c->scheme.group_data_num = -1;
+  c->scheme.chunk_size_bits = -1;
+  ecw_codec_info& in = c->info;
+  in.code_type = 'M';
+  in.node_index = 1;
+  in.encode_data_num = k;
+  in.decode_data_num = k;
+  in.global_num = rows;
+  in.group_data_num = -1;
+  in.parity_num = rows;
+  c->matrix.assign(matrix, matrix + static_cast<size_t>(k) * rows);
+  c->gftbl = isal_tables(k, rows, c->matrix.data());
+  std::vector<uint8_t> ones(256, 1);
+  c->dtbl = isal_tables(k, 1, ones.data());
+  for (int row0 = 0; row0 < rows; row0 += kMaxPassRows)
+    c->pass_img.push_back(packed_pass_tables(c->matrix.data(), k, row0, std::min(kMaxPassRows, rows - row0)));
+  *out = c;
+  return ECW_OK;
+}
+
 int ecw_codec_get_info(const ecw_codec* c, ecw_codec_info* out) {
   if (!c || !out) return ECW_EINVAL;
   *out = c->info;
@@ -693,6 +722,72 @@ int ecw_partial_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target
   if (c->info.partial_decode_num < 1) return ECW_EUNSUPPORTED;
   uint8_t* const out[1] = {target};
   return host_roundtrip(c, data, c->info.partial_decode_num, out, 1, len, op_xor);
+}
+
+// Many stripes from host memory: batches of stripes x column slices go
+// through the same 3-slot / 3-stream pipeline as host_roundtrip, each slot
+// laid out as a slab ([D.., G.., L..] per stripe) so one launch encodes the
+// whole batch.
+int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, uint8_t* const* parity,
+                       size_t len) {
+  if (!c || stripes < 0 || !data || !parity || !check_len(len)) return ECW_EINVAL;
+  if (c->info.multinode) return ECW_EUNSUPPORTED;
+  const int k = c->k(), np = c->info.parity_num, nb = k + np;
+  for (size_t i = 0; i < static_cast<size_t>(stripes) * k; ++i)
+    if (!data[i]) return ECW_EINVAL;
+  for (size_t i = 0; i < static_cast<size_t>(stripes) * np; ++i)
+    if (!parity[i]) return ECW_EINVAL;
+  if (len == 0 || stripes == 0) return ECW_OK;
+  std::lock_guard<std::mutex> lk(c->mu);
+  int st = c->ensure_device();
+  if (st) return st;
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  if (!c->pipe) {
+    c->pipe = new (std::nothrow) HostPipe();
+    if (!c->pipe) return ECW_ENOMEM;
+  }
+  HostPipe& P = *c->pipe;
+  if ((st = P.init())) return st;
+  const size_t chunk = std::min(len, kHostChunk);
+  const size_t cstride = (chunk + 255) & ~static_cast<size_t>(255);
+  const size_t stripe_bytes = cstride * nb;
+  // stripes per batch: fill a slot of ~ (k + np) * 8 MiB
+  const int sb = static_cast<int>(std::max<size_t>(1, std::min<size_t>(stripes, (kHostChunk * nb) / stripe_bytes)));
+  const size_t slot_bytes = stripe_bytes * sb;
+  if ((st = c->ensure_stage(slot_bytes * kSlots))) return st;
+  size_t step = 0;
+  for (int s0 = 0; s0 < stripes; s0 += sb) {
+    const int ns = std::min(sb, stripes - s0);
+    for (size_t c0 = 0; c0 < len; c0 += chunk, ++step) {
+      const int slot = static_cast<int>(step % kSlots);
+      const size_t n = std::min(chunk, len - c0);
+      uint8_t* base = c->d_stage + slot * slot_bytes;
+      if (step >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      for (int s = 0; s < ns; ++s)
+        for (int j = 0; j < k; ++j)
+          if (hipMemcpyAsync(base + s * stripe_bytes + j * cstride, data[static_cast<size_t>(s0 + s) * k + j] + c0, n,
+                             hipMemcpyHostToDevice, P.s_in) != hipSuccess)
+            return ECW_EDEVICE;
+      if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return ECW_EDEVICE;
+      if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      SlabRows slab{base, cstride, stripe_bytes};
+      EncodeTarget t;
+      t.slab = &slab;
+      t.stripes = ns;
+      if ((st = run_encode(c, t, n, P.s_run))) return st;
+      if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return ECW_EDEVICE;
+      if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      for (int s = 0; s < ns; ++s)
+        for (int i = 0; i < np; ++i)
+          if (hipMemcpyAsync(parity[static_cast<size_t>(s0 + s) * np + i] + c0, base + s * stripe_bytes + (k + i) * cstride,
+                             n, hipMemcpyDeviceToHost, P.s_out) != hipSuccess)
+            return ECW_EDEVICE;
+      if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return ECW_EDEVICE;
+    }
+  }
+  if (hipStreamSynchronize(P.s_out) != hipSuccess) return ECW_EDEVICE;
+  return hipStreamSynchronize(P.s_run) == hipSuccess ? ECW_OK : ECW_EDEVICE;
 }
 
 int ecw_repair(ecw_codec* c, const uint8_t* const* blocks, int lost, uint8_t* out, size_t len) {

@@ -52,8 +52,28 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 #define ECW_ABLATE 0  // tuning builds only: 1 = skip the GF lookups, 2 = skip the data loads
 #endif
 
+#ifndef ECW_BUFLOAD
+#define ECW_BUFLOAD 1
+#endif
+
 template <bool TAIL>
 __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
+#if ECW_BUFLOAD
+  // Full tiles: a raw buffer load with the compiler-level volatile bit (aux
+  // bit 31). Without it LLVM sinks the ring's prefetch loads down to their
+  // uses in the next iteration (re-rolling the software pipeline into
+  // "issue P loads, drain"); volatile loads stay where they are written, and
+  // their results are still tracked by the compiler's vmcnt bookkeeping
+  // (counted vmcnt(P-1..0), not vmcnt(0)). Codegen adds sc0 sc1 (L1 bypass,
+  // served from L2): fine for a stream every byte of which is read once.
+  if (!TAIL) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(row), 0, 0x7FFFFFFF, 0x00020000);
+    const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(col), 0, static_cast<int>(0x80000000u));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
+#endif
 #if ECW_ABLATE == 2
   if (!TAIL) return make_uint4(col ^ static_cast<uint32_t>(reinterpret_cast<uintptr_t>(row)), col * 3u, col + 7u, col >> 3);
 #endif
@@ -161,28 +181,51 @@ __device__ __forceinline__ uint4 unpack_row(const uint32_t (&acc)[16 * NW], int 
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+// Column tile `tile` of the slab: stripe, this lane's column, whole tile in range?
+struct TileAt {
+  int s;
+  uint32_t col;
+  bool full;
+};
+
+__device__ __forceinline__ TileAt tile_at(const EncodeGeom& g, uint64_t tile) {
+  const int s = static_cast<int>(tile / g.tiles);
+  const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+  return {s, col0 + threadIdx.x * kLaneBytes, static_cast<uint64_t>(col0) + kTileBytes <= g.len};
+}
+
+// rows 0..P-1 of tile t into the ring (clamped to k-1 when k < P)
+template <int P, bool TAIL, class Rows>
+__device__ __forceinline__ void ring_prologue(uint4 (&ring)[P], const Rows& rows, const EncodeGeom& g,
+                                              const TileAt& t) {
+#pragma unroll
+  for (int p = 0; p < P; ++p)
+    ring[p] = ld16<TAIL>(src_row(rows, g, t.s, p < g.k ? p : g.k - 1), t.col, static_cast<uint32_t>(g.len));
+}
+
+// One column tile: consumes the ring (rows 0..P-1 of `cur` already in flight)
+// and streams rows P..k-1 through it. In the last round of the row loop the
+// slots are refilled with rows 0..P-1 of the next tile when `pf`, so tiles
+// follow each other without a load bubble and without redundant loads.
 template <int NW, int P, int LOCAL, bool TAIL, class Rows>
-__device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& g, int s, uint32_t col,
-                                            uint32_t lds_base) {
+__device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& g, const TileAt& cur,
+                                            uint4 (&ring)[P], bool pf, const TileAt& nxt, uint32_t lds_base) {
   const uint32_t len = static_cast<uint32_t>(g.len);
+  const uint32_t col = cur.col;
   if (TAIL && col >= len) return;
   const int k = g.k;
   uint32_t acc[16 * NW];
 #pragma unroll
   for (int i = 0; i < 16 * NW; ++i) acc[i] = 0;
   uint4 lacc = make_uint4(0, 0, 0, 0);
-  // P-deep prefetch ring. Loads are unconditional (the index is clamped to
-  // k-1 near the end) so every ring slot is a plain load destination.
-  uint4 ring[P];
-#pragma unroll
-  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL>(src_row(rows, g, s, p < k ? p : k - 1), col, len);
   int gend = g.r < k ? g.r : k;
   int t = 0;
   for (int j0 = 0; j0 < k; j0 += P) {
+    const bool last_round = j0 + P >= k;
 #pragma unroll
     for (int p = 0; p < P; ++p) {
-      // consume slot p, then refill it with row j+P: the refill reuses the
-      // slot's registers (no copy, so no early vmcnt wait)
+      // consume slot p, then refill it: the refill reuses the slot's
+      // registers (no copy, so no early vmcnt wait)
       const int j = j0 + p;
       if (j < k) {
 #if ECW_ABLATE == 1
@@ -195,39 +238,63 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
           lacc = xor4(lacc, ring[p]);
           if (j + 1 == gend) {
             const uint4 v = LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0);
-            st16<TAIL>(local_row(rows, g, s, t), col, len, v);
+            st16<TAIL>(local_row(rows, g, cur.s, t), col, len, v);
             lacc = make_uint4(0, 0, 0, 0);
             ++t;
             gend = gend + g.r < k ? gend + g.r : k;
           }
         }
       }
-      const int jn = j + P < k ? j + P : k - 1;
-      ring[p] = ld16<TAIL>(src_row(rows, g, s, jn), col, len);
+      // exactly one load per visit (a conditional load would make the
+      // compiler's vmcnt bookkeeping fall back to vmcnt(0)): the address
+      // selects row j+P of this tile, row p of the next one, or a clamped
+      // re-read of row k-1 when there is nothing left to prefetch
+      const bool use_next = !TAIL && last_round && pf;
+      const int row = use_next ? p : (j + P < k ? j + P : k - 1);
+      ring[p] = ld16<TAIL>(src_row(rows, g, use_next ? nxt.s : cur.s, row), use_next ? nxt.col : col, len);
     }
   }
-  for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, s, l), col, len, unpack_row<NW>(acc, l));
+  for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
 }
 
 template <int NW, int P, int LOCAL, class Rows>
 __global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const EncodeGeom g,
                                                         const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  uint64_t tile = blockIdx.x;
+  uint4 ring[P];
+  // the first tile's row loads are issued before the table staging so the
+  // two overlap
+  bool have = false;
+  if (tile < total) {
+    const TileAt t0 = tile_at(g, tile);
+    if (t0.full) {
+      ring_prologue<P, false>(ring, rows, g, t0);
+      have = true;
+    }
+  }
   const int n16 = g.k * 8 * NW;
   for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
   __syncthreads();
   // dynamic LDS starts at 0 (no static LDS in this kernel); records are
   // 128*NW-byte aligned relative to it
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
-  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
-    const int s = static_cast<int>(tile / g.tiles);
-    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
-    const uint32_t col = col0 + threadIdx.x * kLaneBytes;
-    if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
-      encode_tile<NW, P, LOCAL, false>(rows, g, s, col, lds_base);
-    else
-      encode_tile<NW, P, LOCAL, true>(rows, g, s, col, lds_base);
+  const bool cross = g.k >= P;
+  for (; tile < total; tile += gridDim.x) {
+    const TileAt cur = tile_at(g, tile);
+    if (!cur.full) {
+      ring_prologue<P, true>(ring, rows, g, cur);
+      encode_tile<NW, P, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
+      have = false;
+      continue;
+    }
+    if (!have) ring_prologue<P, false>(ring, rows, g, cur);
+    const uint64_t nt = tile + gridDim.x;
+    const TileAt nxt = tile_at(g, nt < total ? nt : tile);
+    const bool pf = cross && nt < total && nxt.full;
+    encode_tile<NW, P, LOCAL, false>(rows, g, cur, ring, pf, nxt, lds_base);
+    have = pf;
   }
 }
 

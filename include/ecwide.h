@@ -149,6 +149,12 @@ int ecw_scheme_from_ini_text(const char* text, ecw_scheme* out);
 int ecw_codec_create(const ecw_scheme* scheme, int node_index, int multinode, int local_mode,
                      int device, ecw_codec** out);
 void ecw_codec_destroy(ecw_codec* codec);
+/* A codec for an arbitrary rows x k GF(2^8) coefficient matrix (row-major),
+ * no local groups: encode computes parity[l] = sum_j matrix[l][j] * data[j],
+ * exactly ISA-L's ec_encode_data with ec_init_tables(k, rows, matrix)
+ * (isal:erasure_code/ec_highlevel_func.c:33-43; ECWide-H/proxy/encode.cpp:
+ * 129-130, 161-162, 187-188, 222-223 are such calls). code_type 'M'. */
+int ecw_matrix_codec_create(const uint8_t* matrix, int k, int rows, int device, ecw_codec** out);
 int ecw_codec_get_info(const ecw_codec* codec, ecw_codec_info* out);
 int ecw_codec_set_xori_mode(ecw_codec* codec, int xori_mode);
 /* Copy out the m x k encode matrix (row-major), the 32*k*m ISA-L layout
@@ -169,6 +175,13 @@ int ecw_partial_decode(ecw_codec* codec, const uint8_t* const* data, uint8_t* ta
                        size_t len);
 int ecw_xor_intermediate(ecw_codec* codec, const uint8_t* const* source, uint8_t* const* target,
                          size_t len);
+
+/* Encode `stripes` independent stripes held in host memory in one call:
+ * data[s*k + j], parity[s*parity_num + i]. Small blocks (ECWide-H's 4 KiB
+ * chunks) are packed into one HBM slab per batch, so a batch costs one
+ * launch instead of one per stripe. */
+int ecw_encode_stripes(ecw_codec* codec, int stripes, const uint8_t* const* data, uint8_t* const* parity,
+                       size_t len);
 
 /* Flat CL single-block repair on host memory: `blocks` holds every block of
  * one stripe in slab order [D.., G.., L..] (the lost one may be NULL);
