@@ -55,6 +55,9 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 #ifndef ECW_BUFLOAD
 #define ECW_BUFLOAD 1
 #endif
+#ifndef ECW_TILE_ORDER
+#define ECW_TILE_ORDER 0
+#endif
 
 template <bool TAIL>
 __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
@@ -262,12 +265,23 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const E
                                                         const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+#if ECW_TILE_ORDER == 1
+  // contiguous run of tiles per workgroup
+  const uint64_t per = (total + gridDim.x - 1) / gridDim.x;
+  uint64_t tile = blockIdx.x * per;
+  const uint64_t tend = tile + per < total ? tile + per : total;
+  const uint64_t tstep = 1;
+#else
+  // workgroup b takes tiles b, b + grid, b + 2 grid, ...
   uint64_t tile = blockIdx.x;
+  const uint64_t tend = total;
+  const uint64_t tstep = gridDim.x;
+#endif
   uint4 ring[P];
   // the first tile's row loads are issued before the table staging so the
   // two overlap
   bool have = false;
-  if (tile < total) {
+  if (tile < tend) {
     const TileAt t0 = tile_at(g, tile);
     if (t0.full) {
       ring_prologue<P, false>(ring, rows, g, t0);
@@ -281,7 +295,7 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const E
   // 128*NW-byte aligned relative to it
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
   const bool cross = g.k >= P;
-  for (; tile < total; tile += gridDim.x) {
+  for (; tile < tend; tile += tstep) {
     const TileAt cur = tile_at(g, tile);
     if (!cur.full) {
       ring_prologue<P, true>(ring, rows, g, cur);
@@ -290,9 +304,9 @@ __global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const E
       continue;
     }
     if (!have) ring_prologue<P, false>(ring, rows, g, cur);
-    const uint64_t nt = tile + gridDim.x;
-    const TileAt nxt = tile_at(g, nt < total ? nt : tile);
-    const bool pf = cross && nt < total && nxt.full;
+    const uint64_t nt = tile + tstep;
+    const TileAt nxt = tile_at(g, nt < tend ? nt : tile);
+    const bool pf = cross && nt < tend && nxt.full;
     encode_tile<NW, P, LOCAL, false>(rows, g, cur, ring, pf, nxt, lds_base);
     have = pf;
   }

@@ -76,7 +76,7 @@ def main():
             e[2].record()
             torch.cuda.synchronize()
             res[name][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
-            res[name][1].append(rep_bytes * a.iters / max(e[1].elapsed_time(e[2]), 1e-6) / 1e3 / 1e9 * 1e3)
+            res[name][1].append(rep_bytes * a.iters / (max(e[1].elapsed_time(e[2]), 1e-6) * 1e-3) / 1e9)
             if ref is not None and "ablate" not in name:
                 got = buf[(k) * bstride:(k) * bstride + B]
                 if not torch.equal(got, ref):
