@@ -83,8 +83,9 @@ struct ecw_codec {
   bool has_local() const { return info.code_type == 'C' || info.code_type == 'L'; }
   int k() const { return info.encode_data_num; }
   int m() const { return info.global_num; }
-  int groups() const { return has_local() ? info.group_num : 0; }
-  int r() const { return info.group_data_num; }
+  // a multi-node codec encodes one data group: one local parity over all its rows
+  int groups() const { return has_local() ? (info.multinode ? 1 : info.group_num) : 0; }
+  int r() const { return info.multinode ? info.encode_data_num : info.group_data_num; }
 
   // lazily upload the packed tables (first device call)
   int ensure_device() {
@@ -383,9 +384,30 @@ int ecw_codec_create(const ecw_scheme* sch, int node_index, int multinode, int l
     in.rack_per_group = ceil_div(r + 1, rn);
     in.decode_data_num = in.partial_decode_num - 1 + in.rack_per_group - 1;
   }
-  in.parity_num = m + ((t == 'C' || t == 'L') ? in.group_num : 0);
+  in.parity_num = m + ((t == 'C' || t == 'L') ? (multinode ? 1 : in.group_num) : 0);
   const int edn = in.encode_data_num;
-  c->matrix = cauchy_parity_rows(edn, m);
+  if (multinode) {
+    // Multi-node CL encode (ECTaskProcessor.java:267-291, paper p.240 Fig. 6):
+    // node i (1-based) holds data group g-i ("data group 1 - l => node l | ...
+    // | 1", NativeCodec.cc:47) and computes the partial global parities over
+    // that group's columns of the stripe's Cauchy matrix, plus the group's
+    // XOR local parity; xorIntemediate merges partials along the chain. The
+    // reference slices a Cauchy matrix of the GROUP size at a misaligned
+    // offset (NativeCodec.cc:31,46-58: out of bounds for most nodes), so its
+    // partials do not add up to the single-node parities; this implements
+    // the intended columns, whose XOR over all nodes equals encodeData's G.
+    const int c0 = (sch->group_num - node_index) * r;
+    if (c0 < 0) {
+      delete c;
+      return ECW_EINVAL;
+    }
+    const std::vector<uint8_t> full = cauchy_parity_rows(k, m);
+    c->matrix.resize(static_cast<size_t>(edn) * m);
+    for (int l = 0; l < m; ++l)
+      for (int j = 0; j < edn; ++j) c->matrix[static_cast<size_t>(l) * edn + j] = full[static_cast<size_t>(l) * k + c0 + j];
+  } else {
+    c->matrix = cauchy_parity_rows(edn, m);
+  }
   c->gftbl = isal_tables(edn, m, c->matrix.data());
   std::vector<uint8_t> ones(256, 1);
   c->dtbl = isal_tables(in.decode_data_num, 1, ones.data());
@@ -462,7 +484,6 @@ int ecw_codec_partial_decode_gftbl(const ecw_codec* c, uint8_t* out, size_t len)
 int ecw_encode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* const* d_parity, size_t len,
                    void* stream) {
   if (!c || !d_data || !d_parity || !check_len(len)) return ECW_EINVAL;
-  if (c->info.multinode) return ECW_EUNSUPPORTED;
   const int k = c->k(), np = c->info.parity_num;
   if (!all_aligned(d_data, k) || !all_aligned(d_parity, np)) return ECW_EALIGN;
   {
@@ -527,7 +548,6 @@ int ecw_xor_intermediate_dev(ecw_codec* c, const uint8_t* const* d_src, uint8_t*
 int ecw_encode_batch_dev(ecw_codec* c, uint8_t* d_slab, size_t block_stride, size_t stripe_stride, int stripes,
                          size_t len, void* stream) {
   if (!c || !d_slab || stripes < 0 || !check_len(len) || len > block_stride) return ECW_EINVAL;
-  if (c->info.multinode) return ECW_EUNSUPPORTED;
   if (!aligned16(d_slab) || block_stride % 16 || stripe_stride % 16) return ECW_EALIGN;
   const size_t nblk = static_cast<size_t>(c->k()) + c->info.parity_num;
   if (stripes > 1 && stripe_stride < nblk * block_stride) return ECW_EINVAL;
@@ -707,7 +727,6 @@ static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout
 
 int ecw_encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
   if (!c || !data || !parity || !check_len(len)) return ECW_EINVAL;
-  if (c->info.multinode) return ECW_EUNSUPPORTED;
   return host_roundtrip(c, data, c->k(), parity, c->info.parity_num, len, op_encode);
 }
 
@@ -731,7 +750,6 @@ int ecw_partial_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target
 int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, uint8_t* const* parity,
                        size_t len) {
   if (!c || stripes < 0 || !data || !parity || !check_len(len)) return ECW_EINVAL;
-  if (c->info.multinode) return ECW_EUNSUPPORTED;
   const int k = c->k(), np = c->info.parity_num, nb = k + np;
   for (size_t i = 0; i < static_cast<size_t>(stripes) * k; ++i)
     if (!data[i]) return ECW_EINVAL;

@@ -141,8 +141,13 @@ int ecw_scheme_from_ini_text(const char* text, ecw_scheme* out);
 
 /* ---- codec ------------------------------------------------------------ */
 /* Create a codec for `scheme` as seen from 1-based `node_index`.
- * `multinode` selects the multi-node partial-encode geometry; only its
- * counts are supported (encode with multinode=1 returns ECW_EUNSUPPORTED).
+ * `multinode` selects the multi-node partial encode (ECTaskProcessor.java:
+ * 267-291): node i holds data group g-i, encode writes the m partial global
+ * parities over that group's columns of the stripe's Cauchy matrix plus the
+ * group's local parity (m+1 outputs); XOR-merging the partials of all nodes
+ * (xorIntemediate) gives the single-node global parities. The reference's
+ * own column slice is misaligned (NativeCodec.cc:46-58), so this mode
+ * implements the intended columns.
  * `device` is the HIP device ordinal used for every device-side call;
  * no device work happens until the first encode/decode call, so a codec can
  * be created (and its matrices inspected) on a host without a GPU. */

@@ -214,6 +214,37 @@ def test_host_pipeline_multi_chunk_and_repair(E, torch, orc, B):
         assert np.array_equal(out, blocks[lost]), lost
 
 
+@pytest.mark.parametrize("k,m,r,B", [(32, 3, 11, 65536 + 16), (128, 3, 27, 1 << 16), (20, 2, 5, 4096)])
+def test_multinode_encode_chain(E, torch, orc, k, m, r, B):
+    """Multi-node CL encode (ECTaskProcessor.java:267-291): each of the g
+    nodes encodes its own group on the GPU, partials are merged along the
+    chain with xorIntemediate; the result equals single-node encodeData
+    (the oracle), and each node's local parity is its group's XOR. (The
+    reference's own slice is misaligned, so this is pinned to the
+    single-node code, not to a reference multi-node run.)"""
+    s = E.CodingScheme.getClScheme(k, m, r, B)
+    g = s.groupNum
+    data = [orc.fill(B, 21, 0, j) for j in range(k)]
+    want = orc.codec("C", k, m, r, B).encode(data, threads=8)
+    chain = None
+    for node in range(1, g + 1):
+        c = E.NativeCodec.getClCodec(s, node, True)
+        c0 = (g - node) * r
+        mine = [torch.from_numpy(d).cuda() for d in data[c0:c0 + c.encodeDataNum]]
+        par = [torch.zeros(B, dtype=torch.uint8, device="cuda") for _ in range(m + 1)]
+        c.encodeData(mine, par)
+        torch.cuda.synchronize()
+        t = c0 // r
+        assert np.array_equal(par[m].cpu().numpy(), want[m + t]), ("local", node)
+        if chain is None:
+            chain = par[:m]
+        else:
+            c.xorIntemediate(par[:m], chain)  # chain ^= this node's partials
+    torch.cuda.synchronize()
+    for i in range(m):
+        assert np.array_equal(chain[i].cpu().numpy(), want[i]), i
+
+
 def test_literal_mode_slab_writes_zero_locals(E, torch):
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(32, 2, 8, 65536), 1, False, local_mode="literal")
     slab = E.StripeSlab(c, stripes=2, block_bytes=65536)

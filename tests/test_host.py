@@ -123,11 +123,28 @@ def test_errors():
         E.CodingScheme.getClScheme(250, 7, 10, 64)  # k + m > 256
     with pytest.raises(E.EcwError):
         E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(4, 2, 64)).repairSources(0)  # no local groups
-    c = E.NativeCodec(s, 1, True)  # multi-node geometry: counts only
-    assert c.encodeDataNum == 4
-    with pytest.raises(E.EcwError) as ei:
-        c.encodeData([np.zeros(64, np.uint8)] * 4, [np.zeros(64, np.uint8)] * 4)
-    assert ei.value.status == -5
+    c = E.NativeCodec(s, 1, True)  # multi-node: node 1 holds the last group
+    assert (c.encodeDataNum, c.parityNum) == (4, 3)
+    with pytest.raises(E.EcwError):
+        E.NativeCodec(s, 3, True)  # only groupNum (= 2) encode nodes exist
+
+
+def test_multinode_matrix_columns(orc):
+    """Node i's partial-parity matrix = columns of group g-i of the stripe's
+    Cauchy rows (ClMetadataManager.getMultinodeEncodeTask runs nodes 1..g)."""
+    k, m, r = 32, 3, 11
+    s = E.CodingScheme.getClScheme(k, m, r, 64)
+    full = orc.cauchy1(k + m, k)[k:]
+    g = s.groupNum
+    cols = []
+    for node in range(1, g + 1):
+        c = E.NativeCodec(s, node, True)
+        c0 = (g - node) * r
+        assert c.encodeDataNum == (k - c0 if node == 1 else r)
+        mat = c.getEncodeMatrix().reshape(m, c.encodeDataNum)
+        assert np.array_equal(mat, full[:, c0:c0 + c.encodeDataNum])
+        cols += list(range(c0, c0 + c.encodeDataNum))
+    assert sorted(cols) == list(range(k))
 
 
 @pytest.mark.skipif(E.device_count() > 0, reason="checks the no-GPU failure mode")
