@@ -52,14 +52,19 @@ def dist_setup(args):
     from ecwide_amd.shard import dist_env
 
     world, rank, local = dist_env()
+    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of
+    # the N>1 path) ranks share devices and the timing collective runs on gloo
+    ndev = max(1, torch.cuda.device_count())
+    dev = local % ndev
+    torch.cuda.set_device(dev)
     if world > 1:
         import torch.distributed as dist
 
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
-    else:
-        torch.cuda.set_device(0)
-    return world, rank, local
+        if ndev >= world:
+            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
+        else:
+            dist.init_process_group("gloo")
+    return world, rank, dev
 
 
 def barrier(world):
@@ -75,7 +80,8 @@ def max_over_ranks(world, x: float) -> float:
     import torch
     import torch.distributed as dist
 
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    on_gpu = dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 

@@ -158,3 +158,22 @@ def test_device_calls_fail_loudly_without_gpu():
 def test_status_strings():
     for st in range(0, -8, -1):
         assert _lib.lib.ecw_status_string(st)
+
+
+def test_chunk_generator_names():
+    """generateChunks naming (ChunkGenerator.java:59-103) for the default
+    scheme: toy names carry the 1-based node position of the CL layout."""
+    from ecwide_amd.chunk_generator import chunk_file_names
+
+    s = E.CodingScheme.fromConfigText(DEFAULT_INI)
+    toy = chunk_file_names(s, -1)
+    assert len(toy) == 32 + 3 + 3
+    assert toy[:3] == ["1_D_0", "2_D_1", "3_D_2"]
+    assert toy[10:13] == ["11_D_10", "13_D_11", "14_D_12"]  # group boundary skips L's position
+    assert toy[31] == "34_D_31"
+    assert toy[32:35] == ["36_G_0", "37_G_1", "38_G_2"]
+    assert toy[35:] == ["12_L_0", "24_L_1", "35_L_2"]
+    st = chunk_file_names(s, 7)
+    assert st[0] == "D_7_0" and st[32] == "G_7_0" and st[-1] == "L_7_2"
+    rs = chunk_file_names(E.CodingScheme.getRsScheme(4, 2, 64), -1)
+    assert rs == ["1_D_0", "2_D_1", "3_D_2", "4_D_3", "5_G_0", "6_G_1"]
