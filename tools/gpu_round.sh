@@ -1,4 +1,6 @@
-# One GPU round: parity tests, smoke, bench, rocprof kernel stats, PMC traffic.
+# One GPU round: parity tests, smoke, bench, rocprof kernel stats, PMC traffic,
+# host-resident (PCIe) rate. Every GPU step has its own time limit; the
+# script stops at the first failure.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 TAG=${TAG:-r01}
 nproc > gpurun_out/host.txt; lscpu >> gpurun_out/host.txt 2>&1
@@ -14,5 +16,5 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_fetch_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc1.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_write_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc2.log 2>&1 || exit $?
 echo "profiles done"
-#cd $GRAFT_REPO_ROOT && timeout -k 10 400 python bench.py --host-resident --steps 12 > gpurun_out/bench_host.log 2>&1 || exit $?
+cd $GRAFT_REPO_ROOT && timeout -k 10 400 python bench.py --host-resident --steps 12 > gpurun_out/bench_host.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_host.log
