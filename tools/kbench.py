@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--iters", type=int, default=5)
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--code", default="C", help="C (CL, locals) or R (RS, globals only)")
+    ap.add_argument("--pad", type=int, default=4096, help="block stride = B + pad (rounded to 256)")
     a = ap.parse_args()
     import torch
 
@@ -36,7 +37,7 @@ def main():
     B = int(a.mib * (1 << 20))
     g = -(-k // r) if a.code == "C" else 0
     nblk = k + m + g
-    bstride = (B + 4096 + 255) // 256 * 256
+    bstride = (B + a.pad + 255) // 256 * 256
     sstride = nblk * bstride
     S = a.stripes
     buf = torch.empty(S * sstride, dtype=torch.uint8, device="cuda")
