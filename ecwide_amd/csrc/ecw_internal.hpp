@@ -43,6 +43,8 @@ struct EncodeGeom {
   int m;                 // total global rows (slab output indexing)
   int row0, nrows;       // global rows of this pass [row0, row0 + nrows)
   int local_mode;        // LocalMode
+  uint64_t tile_begin;   // this launch covers slab tiles [tile_begin, tile_end)
+  uint64_t tile_end;     //   (tile = stripe * tiles + column tile)
 };
 
 // Launchers return hipSuccess or the launch error.
