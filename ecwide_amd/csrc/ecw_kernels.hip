@@ -389,15 +389,18 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
 #define ECW_PREFETCH_XOR 8
 #endif
 #ifndef ECW_GRID_PER_CU
-#define ECW_GRID_PER_CU 64
+#define ECW_GRID_PER_CU 64  // encode: workgroups per CU before tiles are grid-strided
+#endif
+#ifndef ECW_GRID_PER_CU_XOR
+#define ECW_GRID_PER_CU_XOR 512  // XOR reduce: one workgroup per tile (measured +7.7 %)
 #endif
 constexpr int kPrefetchEnc = ECW_PREFETCH_ENC;
 constexpr int kPrefetchXor = ECW_PREFETCH_XOR;
 
-unsigned grid_for(uint64_t tiles_total) {
-  // memory-bound streaming: enough workgroups to fill 256 CUs several deep,
-  // grid-stride for the rest (tables are staged once per workgroup)
-  const uint64_t cap = 256ull * ECW_GRID_PER_CU;
+unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
+  // memory-bound streaming: enough workgroups to fill 256 CUs many deep,
+  // grid-stride beyond that (encode tables are staged once per workgroup)
+  const uint64_t cap = 256ull * per_cu;
   return static_cast<unsigned>(tiles_total < cap ? (tiles_total ? tiles_total : 1) : cap);
 }
 
@@ -445,7 +448,8 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
   if (total == 0) return hipSuccess;
   if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), dim3(grid_for(total)), dim3(kBlock), 0, s, a, g);
+  hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), dim3(grid_for(total, ECW_GRID_PER_CU_XOR)), dim3(kBlock), 0,
+                     s, a, g);
   return hipGetLastError();
 }
 
