@@ -45,6 +45,9 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 // Columns are 32-bit offsets from a wave-uniform row pointer, so loads and
 // stores use the SGPR-base + VGPR-offset form (blocks are < 4 GiB; the host
 // checks it).
+#ifndef ECW_NT_STORES
+#define ECW_NT_STORES 0
+#endif
 #ifndef ECW_NT_LOADS
 #define ECW_NT_LOADS 0
 #endif
@@ -96,7 +99,13 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t
 template <bool TAIL>
 __device__ __forceinline__ void st16(uint8_t* row, uint32_t col, uint32_t len, uint4 v) {
   if (!TAIL || col + 16 <= len) {
+#if ECW_NT_STORES
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 w = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(row + col));
+#else
     *reinterpret_cast<uint4*>(row + col) = v;
+#endif
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -203,6 +212,20 @@ __device__ __forceinline__ void ring_prologue(uint4 (&ring)[P], const Rows& rows
     ring[p] = ld16<TAIL>(src_row(rows, g, t.s, p < g.k ? p : g.k - 1), t.col, static_cast<uint32_t>(g.len));
 }
 
+#ifndef ECW_LOCAL_LDS
+#define ECW_LOCAL_LDS 0
+#endif
+constexpr int kMaxLdsLocals = 8;  // local parities staged in LDS per tile (4 KiB each)
+
+// Local parities are staged in LDS (after the tables) when the launch has
+// few enough groups; the host sizes the dynamic LDS with the same rule.
+__host__ __device__ __forceinline__ bool stage_locals(const EncodeGeom& g) {
+  return ECW_LOCAL_LDS && g.local_mode != kLocalNone && g.groups <= kMaxLdsLocals;
+}
+__device__ __forceinline__ uint32_t loc_base(const EncodeGeom& g, uint32_t lds_base) {
+  return lds_base + static_cast<uint32_t>(g.k) * 128u * (g.nrows <= 4 ? 1u : 2u);
+}
+
 // One column tile: consumes the ring (rows 0..P-1 of `cur` already in flight)
 // and streams rows P..k-1 through it. In the last round of the row loop the
 // slots are refilled with rows 0..P-1 of the next tile when `pf`, so tiles
@@ -238,7 +261,18 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
           lacc = xor4(lacc, ring[p]);
           if (j + 1 == gend) {
             const uint4 v = LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0);
-            st16<TAIL>(local_row(rows, g, cur.s, t), col, len, v);
+            if (!TAIL && stage_locals(g)) {
+              // park the finished local parity in LDS; the global store is
+              // issued with the global parities at the end of the tile (a
+              // store here would sit in vmcnt ahead of the next row's loads)
+              typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+              typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
+              const u32x4 w = {v.x, v.y, v.z, v.w};
+              *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(
+                  loc_base(g, lds_base) + t * kTileBytes + threadIdx.x * kLaneBytes)) = w;
+            } else {
+              st16<TAIL>(local_row(rows, g, cur.s, t), col, len, v);
+            }
             lacc = make_uint4(0, 0, 0, 0);
             ++t;
             gend = gend + g.r < k ? gend + g.r : k;
@@ -255,10 +289,24 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
     }
   }
   for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
+  if constexpr (LOCAL != kLocalNone) {
+    if (!TAIL && stage_locals(g)) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
+      for (int u = 0; u < g.groups; ++u) {
+        const u32x4 w = *reinterpret_cast<lds_cu32x4*>(static_cast<uintptr_t>(
+            loc_base(g, lds_base) + u * kTileBytes + threadIdx.x * kLaneBytes));
+        st16<false>(local_row(rows, g, cur.s, u), col, len, make_uint4(w.x, w.y, w.z, w.w));
+      }
+    }
+  }
 }
 
 template <int NW, int P, int LOCAL, class Rows>
-__global__ __launch_bounds__(kBlock) void encode_kernel(const Rows rows, const EncodeGeom g,
+#ifndef ECW_ENC_MIN_WAVES
+#define ECW_ENC_MIN_WAVES 6  // __launch_bounds__ min waves per SIMD: caps VGPRs at 80 (+1-4 %; spills only outside the row loop)
+#endif
+__global__ __launch_bounds__(kBlock, ECW_ENC_MIN_WAVES) void encode_kernel(const Rows rows, const EncodeGeom g,
                                                         const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // workgroup b takes tiles begin + b, + grid, + 2 grid, ... (concurrently
@@ -406,7 +454,7 @@ unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
 
 template <int NW, class Rows>
 hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
-  const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + (stage_locals(g) ? size_t(g.groups) * kTileBytes : 0);
   switch (g.local_mode) {
     case kLocalXor:
       hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
