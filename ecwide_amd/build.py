@@ -1,7 +1,9 @@
 """Build libecwide.so (HIP kernels + C ABI) and libecw_isal.so (the ISA-L
-signature shim over it) in-tree: hipcc, gfx950 only."""
+signature shim over it) in-tree: hipcc, gfx950 only. libcodec.so (the JNI
+natives of ECWide-C over the C ABI) is built when a JDK's jni.h is found."""
 from __future__ import annotations
 
+import glob
 import os
 import subprocess
 import sys
@@ -38,6 +40,39 @@ def build(force: bool = False) -> str:
         subprocess.run(cmd, check=True)
         os.replace(SHIM_OUT + ".tmp", SHIM_OUT)
     return OUT
+
+
+JNI_SRC = os.path.join(HERE, "csrc", "jni", "ecw_jni.cpp")
+JNI_OUT = os.path.join(HERE, "libcodec.so")
+
+
+def jdk_include_dirs() -> list[str] | None:
+    """$JAVA_HOME/include (+ include/linux), else the first /usr/lib/jvm JDK."""
+    homes = [os.environ["JAVA_HOME"]] if os.environ.get("JAVA_HOME") else []
+    homes += sorted(glob.glob("/usr/lib/jvm/*"))
+    for h in homes:
+        inc = os.path.join(h, "include")
+        if os.path.exists(os.path.join(inc, "jni.h")):
+            return [inc, os.path.join(inc, "linux")]
+    return None
+
+
+def build_jni(include_dirs: list[str] | None = None, out: str = JNI_OUT, force: bool = False) -> str | None:
+    """libcodec.so: ECWide-C's Java_NativeCodec_* over libecwide.so. Returns its
+    path, or None when no jni.h is available (this image has no JDK)."""
+    include_dirs = include_dirs or jdk_include_dirs()
+    if not include_dirs:
+        return None
+    build()
+    if force or not up_to_date(out, [JNI_SRC, OUT]):
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+        rpath = os.path.relpath(HERE, os.path.dirname(os.path.abspath(out)))
+        cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
+               *("-I" + d for d in include_dirs), "-I" + os.path.join(REPO, "include"), JNI_SRC,
+               "-L" + HERE, "-lecwide", "-Wl,-rpath,$ORIGIN/" + rpath, "-o", out + ".tmp"]
+        subprocess.run(cmd, check=True)
+        os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

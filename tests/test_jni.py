@@ -1,0 +1,275 @@
+"""libcodec.so — the JNI drop-in for ECWide-C (`ECWide-C/src/native/NativeCodec.h:15-72`,
+loaded by `NativeCodec.java:213-215`) — compiled from ecwide_amd/csrc/jni/ecw_jni.cpp
+against a test double of the JNI interface (tests/jni/, no JDK in this image) and
+driven the way the Java constructors and ComputeTask drive it. NativeCodec-like
+objects carry the field values the reference constructors compute (the golden
+fixtures' `fields`, NativeCodec.java:20-109)."""
+import ctypes
+import hashlib
+import importlib.util
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import REPO, golden_blocks
+
+OUT = os.path.join(REPO, "build", "test_jni")
+NATIVES = ["generateEncodeMatrix", "initEncodeTable", "initDecodeTable", "initPartialDecodeTable",
+           "encodeData", "decodeData", "partialDecodeData", "xorIntemediate"]  # NativeCodec.h:15-72
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+class JNI:
+    def __init__(self, shim, dbl):
+        self.shim, self.dbl = shim, dbl
+        vp = ctypes.c_void_p
+        dbl.jd_env.restype = vp
+        dbl.jd_object.restype = vp
+        dbl.jd_object.argtypes = [ctypes.c_char_p]
+        dbl.jd_set_prim.argtypes = [vp, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_longlong]
+        dbl.jd_set_object.argtypes = [vp, ctypes.c_char_p, vp]
+        dbl.jd_buffer.restype = vp
+        dbl.jd_buffer.argtypes = [vp, ctypes.c_longlong]
+        dbl.jd_array.restype = vp
+        dbl.jd_array.argtypes = [ctypes.c_int]
+        dbl.jd_array_set.argtypes = [vp, ctypes.c_int, vp]
+        dbl.jd_exception.restype = ctypes.c_char_p
+        dbl.jd_live_refs.restype = ctypes.c_longlong
+        for n in NATIVES:
+            fn = getattr(shim, "Java_NativeCodec_" + n)
+            fn.restype = None
+            fn.argtypes = [vp, vp] + ([vp, vp] if n in ("encodeData", "decodeData", "partialDecodeData",
+                                                         "xorIntemediate") else [])
+        self.env = dbl.jd_env()
+
+    def call(self, name, obj, *args):
+        self.dbl.jd_clear_exception()
+        getattr(self.shim, "Java_NativeCodec_" + name)(self.env, obj, *args)
+        return self.dbl.jd_exception().decode()
+
+    def buffer(self, arr):
+        return self.dbl.jd_buffer(arr.ctypes.data, arr.nbytes)
+
+    def array(self, arrs):
+        a = self.dbl.jd_array(len(arrs))
+        for i, x in enumerate(arrs):
+            self.dbl.jd_array_set(a, i, self.buffer(x) if x is not None else None)
+        return a
+
+
+class JavaCodec:
+    """A NativeCodec object as its Java constructor leaves it: typed fields,
+    direct buffers of the sizes the ctor allocates, then the ctor's init natives
+    (NativeCodec.java:20-109)."""
+
+    def __init__(self, j: JNI, f: dict, chunk: int, multinode: bool = False, init: bool = True):
+        self.j, self.f, self.chunk = j, f, chunk
+        t = f["code_type"]
+        o = self.o = j.dbl.jd_object(b"NativeCodec")
+        edn, m, ddn, pdn = f["edn"], f["m"], f["ddn"], f.get("pdn", 0)
+        ints = {"chunkSize": chunk, "encodeDataNum": edn, "decodeDataNum": ddn, "partialDecodeNum": pdn,
+                "globalNum": m, "groupNum": max(f.get("group_num", 0), 0),
+                "groupDataNum": max(f.get("r", 0), 0), "rackPerGroup": f.get("rack_per_group", 0),
+                # the RS and LRC ctors never assign nodeIndex (NativeCodec.java:20-31,56-73)
+                "nodeIndex": 0 if t in "RL" else f["node"]}
+        for name, v in ints.items():
+            j.dbl.jd_set_prim(o, name.encode(), b"I", v)
+        j.dbl.jd_set_prim(o, b"codeType", b"C", ord(t))
+        j.dbl.jd_set_prim(o, b"multiNodeEncode", b"Z", int(multinode))
+        self.matrix = np.zeros(edn * m, np.uint8)
+        self.gftbl = np.zeros(32 * edn * m, np.uint8)
+        self.dtbl = np.zeros(32 * ddn, np.uint8)
+        self.pdtbl = np.zeros(32 * pdn, np.uint8) if t in "TC" else None
+        for name, arr in [("encodeMatrix", self.matrix), ("encodeGftbl", self.gftbl), ("decodeGftbl", self.dtbl),
+                          ("partialDecodeGftbl", self.pdtbl)]:
+            j.dbl.jd_set_object(o, name.encode(), j.buffer(arr) if arr is not None else None)
+        self.parity_num = m + (f["group_num"] if t in "CL" and not multinode else (1 if multinode else 0))
+        if init:
+            for n in NATIVES[:3] + (NATIVES[3:4] if t in "TC" else []):
+                assert self.j.call(n, o) == "", n
+
+    def encode(self, data, parity):
+        return self.j.call("encodeData", self.o, self.j.array(data), self.j.array(parity))
+
+    def decode(self, data, target, partial=False):
+        return self.j.call("partialDecodeData" if partial else "decodeData", self.o, self.j.array(data),
+                           self.j.buffer(target))
+
+    def xori(self, src, tgt):
+        return self.j.call("xorIntemediate", self.o, self.j.array(src), self.j.array(tgt))
+
+
+def oracle_fields(orc, k, m, r, B, node):
+    """CL NativeCodec field values for node `node` (single-node geometry), from the oracle."""
+    oc = orc.codec("C", k, m, r, B, node=node)
+    return {"code_type": "C", "edn": oc.encode_data_num, "m": m, "ddn": oc.decode_data_num,
+            "pdn": oc.partial_decode_num, "group_num": oc.group_num, "r": r, "node": node,
+            "rack_per_group": oc.rack_per_group}
+
+
+def _builder():
+    spec = importlib.util.spec_from_file_location("ecw_build", os.path.join(REPO, "ecwide_amd", "build.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+@pytest.fixture(scope="module")
+def jni():
+    import ecwide_amd  # noqa: F401  (torch-first runtime order, then libecwide.so)
+
+    double_dir = os.path.join(REPO, "tests", "jni")
+    shim = _builder().build_jni([double_dir], out=os.path.join(OUT, "libcodec.so"))
+    dbl = os.path.join(OUT, "libjvm_double.so")
+    src = os.path.join(double_dir, "jvm_double.cpp")
+    if not os.path.exists(dbl) or os.path.getmtime(dbl) < max(os.path.getmtime(src),
+                                                               os.path.getmtime(os.path.join(double_dir, "jni.h"))):
+        subprocess.run(["g++", "-O1", "-std=c++17", "-fPIC", "-shared", "-I" + double_dir, src, "-o", dbl],
+                       check=True)
+    return JNI(ctypes.CDLL(shim), ctypes.CDLL(dbl))
+
+
+def test_exports_the_eight_natives(jni):
+    out = subprocess.run(["nm", "-D", "--defined-only", os.path.join(OUT, "libcodec.so")], capture_output=True,
+                         text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if " T " in ln}
+    assert {"Java_NativeCodec_" + n for n in NATIVES} <= exported
+    assert not [s for s in exported if s.startswith("_Z")], "only the JNI natives are exported"
+
+
+def test_ctor_tables_match_oracle(jni, orc, manifest):
+    """The four init natives fill the Java-owned buffers exactly as the
+    reference (NativeCodec.cc:12-135): Cauchy rows, ec_init_tables layout,
+    all-ones decode tables."""
+    for e in manifest["encode"]:
+        f = e["fields"]
+        c = JavaCodec(jni, f, e["len"])
+        oc = orc.codec(e["code_type"], e["k"], e["m"], max(e["r"], 1), e["len"])
+        assert np.array_equal(c.matrix, oc.encode_matrix().ravel()), e["name"]
+        assert np.array_equal(c.gftbl, oc.encode_gftbl().ravel()), e["name"]
+        assert np.array_equal(c.dtbl, orc.init_tables(f["ddn"], 1, np.ones(f["ddn"], np.uint8)).ravel())
+        if c.pdtbl is not None:
+            assert np.array_equal(c.pdtbl, orc.init_tables(f["pdn"], 1, np.ones(f["pdn"], np.uint8)).ravel())
+
+
+def test_local_refs_released(jni, manifest):
+    e = manifest["encode"][0]
+    before = jni.dbl.jd_live_refs()
+    JavaCodec(jni, e["fields"], e["len"])
+    assert jni.dbl.jd_live_refs() == before
+
+
+def test_errors_raise_java_exceptions(jni, manifest):
+    """Where the reference would crash the JVM (short arrays, missing buffers) the
+    shim throws; nothing reaches the device."""
+    e = manifest["encode"][0]
+    f, B = e["fields"], e["len"]
+    c = JavaCodec(jni, f, B)
+    data = [np.zeros(B, np.uint8) for _ in range(f["edn"] - 1)]  # one short
+    par = [np.zeros(B, np.uint8) for _ in range(c.parity_num)]
+    assert c.encode(data, par).startswith("java/lang/IllegalArgumentException")
+    data.append(None)  # a null element
+    assert c.encode(data, par).startswith("java/lang/IllegalArgumentException")
+    data[-1] = np.zeros(B // 2, np.uint8)  # smaller than chunkSize
+    assert "chunkSize" in c.encode(data, par)
+    assert c.decode(data[:1], np.zeros(B, np.uint8)).startswith("java/lang/IllegalArgumentException")
+    # counts that disagree with the codec geometry (a corrupted object)
+    bad = dict(f, ddn=f["ddn"] + 1)
+    b = JavaCodec(jni, bad, B, init=False)
+    assert jni.call("initDecodeTable", b.o).startswith("java/lang/IllegalStateException")
+    # a field the class does not have (wrong signature): NoSuchFieldError passes through
+    o = jni.dbl.jd_object(b"NativeCodec")
+    jni.dbl.jd_set_prim(o, b"chunkSize", b"J", B)
+    assert jni.call("generateEncodeMatrix", o).startswith("java/lang/NoSuchFieldError")
+    # CL multi-node on node > 1 needs k
+    os.environ.pop("ECWIDE_K", None)
+    mf = dict(f, node=2, edn=f["r"])
+    mc = JavaCodec(jni, mf, B, multinode=True, init=False)
+    assert jni.call("generateEncodeMatrix", mc.o).startswith("java/lang/IllegalStateException")
+
+
+@pytest.mark.gpu
+def test_xori_literal_first_call(jni, orc, manifest, monkeypatch):
+    """ECWIDE_XORI_LITERAL=1: the process's first xorIntemediate writes zeros, the
+    next ones XOR (NativeCodec.cc:284-323, static `flag`). Must be the first
+    xorIntemediate through this library in the process (it is: file order)."""
+    e = manifest["xor_intermediate"]
+    m, ln = e["m"], e["len"]
+    s1, s2, s3 = e["seeds"]
+    src1 = [orc.fill(ln, s1, 0, j) for j in range(m)]
+    tgt = [orc.fill(ln, s2, 0, j) for j in range(m)]
+    src2 = [orc.fill(ln, s3, 0, j) for j in range(m)]
+    monkeypatch.setenv("ECWIDE_XORI_LITERAL", "1")
+    c = JavaCodec(jni, oracle_fields(orc, 8, m, 4, ln, 1), ln)
+    assert c.xori(src1, tgt) == ""
+    assert [sha(x) for x in tgt] == e["first"]
+    assert c.xori(src2, tgt) == ""
+    want = golden_blocks(e["second"], m, ln)
+    assert all(np.array_equal(a, b) for a, b in zip(tgt, want))
+
+
+@pytest.mark.gpu
+def test_encode_golden_both_local_modes(jni, orc, manifest, monkeypatch):
+    for e in manifest["encode"]:
+        f, B = e["fields"], e["len"]
+        data = [orc.fill(B, e["seed"], 0, j) for j in range(e["k"])]
+        monkeypatch.delenv("ECWIDE_LOCAL_MODE", raising=False)
+        c = JavaCodec(jni, f, B)
+        par = [np.full(B, 0x5A, np.uint8) for _ in range(c.parity_num)]
+        assert c.encode(data, par) == "", e["name"]
+        want = golden_blocks(e["xor"], c.parity_num, B)
+        assert all(np.array_equal(g, w) for g, w in zip(par, want)), e["name"]
+        if e["code_type"] in "CL":
+            monkeypatch.setenv("ECWIDE_LOCAL_MODE", "literal")
+            c2 = JavaCodec(jni, f, B)
+            par2 = [np.full(B, 0xAB, np.uint8) for _ in range(c2.parity_num)]
+            assert c2.encode(data, par2) == ""
+            assert [sha(x) for x in par2] == e["literal_sha256"], e["name"]
+
+
+@pytest.mark.gpu
+def test_decode_and_partial_decode(jni, orc):
+    """Requestor and relayer stages at the (136,128,27) geometry: ddn 9, pdn 4."""
+    B = 1 << 20
+    f = oracle_fields(orc, 128, 3, 27, B, 1)
+    assert (f["ddn"], f["pdn"]) == (9, 4)
+    c = JavaCodec(jni, f, B)
+    data = [orc.fill(B, 60, 0, j) for j in range(9)]
+    t = np.zeros(B, np.uint8)
+    assert c.decode(data, t) == ""
+    assert np.array_equal(t, orc.xor_blocks(data))
+    assert c.decode(data[:4], t, partial=True) == ""
+    assert np.array_equal(t, orc.xor_blocks(data[:4]))
+
+
+@pytest.mark.gpu
+def test_multinode_chain_equals_single_node(jni, orc, monkeypatch):
+    """ECTaskProcessor.java:267-291 through the JNI natives: every node encodes its
+    group's partial globals + local parity, xorIntemediate merges the partials
+    along the chain; the merged globals equal single-node encodeData."""
+    k, m, r, B = 20, 3, 6, 8192
+    g = -(-k // r)
+    monkeypatch.setenv("ECWIDE_K", str(k))
+    data = [orc.fill(B, 70, 0, j) for j in range(k)]
+    single = JavaCodec(jni, oracle_fields(orc, k, m, r, B, 1), B)
+    want = [np.zeros(B, np.uint8) for _ in range(single.parity_num)]
+    assert single.encode(data, want) == ""
+    acc = None
+    for node in range(1, g + 1):
+        grp = g - node
+        cols = list(range(grp * r, min(k, (grp + 1) * r)))
+        f = dict(oracle_fields(orc, k, m, r, B, node), edn=len(cols))  # NativeCodec.java:84-91
+        c = JavaCodec(jni, f, B, multinode=True)
+        out = [np.zeros(B, np.uint8) for _ in range(m + 1)]
+        assert c.encode([data[j] for j in cols], out) == ""
+        assert np.array_equal(out[m], want[m + grp]), node  # the group's local parity
+        if acc is None:
+            acc = out[:m]
+        else:
+            assert c.xori(out[:m], acc) == ""
+    assert all(np.array_equal(a, w) for a, w in zip(acc, want[:m]))

@@ -1,4 +1,9 @@
 cd $GRAFT_REPO_ROOT
 V=build/variants
-timeout -k 10 300 python tools/kbench.py --stripes 8 --rounds 4 --check $V/base.so $V/lds.so $V/nts.so $V/w6.so $V/w6lds.so 2>&1 | grep -v amdgpu | tail -6 || exit $?
-timeout -k 10 300 python tools/kbench.py --stripes 8 --rounds 3 --code R $V/base.so $V/w6.so 2>&1 | grep -v amdgpu | tail -3 || exit $?
+K="timeout -k 10 240 python tools/kbench.py --stripes 8 --rounds 3 $V/base.so"
+$K 2>&1 | grep -v amdgpu | tail -2 &&
+$K --chunk 1048576 --pad 0 2>&1 | grep -v amdgpu | tail -2 &&
+$K --chunk 262144 --pad 0 2>&1 | grep -v amdgpu | tail -2 &&
+$K --chunk 65536 --pad 0 2>&1 | grep -v amdgpu | tail -2 &&
+$K --chunk 65536 --pad 4096 2>&1 | grep -v amdgpu | tail -2 &&
+$K --chunk 16384 --pad 0 2>&1 | grep -v amdgpu | tail -2

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--code", default="C", help="C (CL, locals) or R (RS, globals only)")
     ap.add_argument("--pad", type=int, default=4096, help="block stride = B + pad (rounded to 256)")
+    ap.add_argument("--chunk", type=int, default=0,
+                    help="chunk-interleaved layout: each stripe stored as B/CHUNK column chunks, "
+                         "the k+m+g blocks' chunks adjacent (timed as B/CHUNK mini-stripes)")
     a = ap.parse_args()
     import torch
 
@@ -35,11 +38,14 @@ def main():
 
     k, m, r = a.k, a.m, a.r
     B = int(a.mib * (1 << 20))
+    S = a.stripes
+    if a.chunk:
+        assert B % a.chunk == 0
+        S, B = S * (B // a.chunk), a.chunk
     g = -(-k // r) if a.code == "C" else 0
     nblk = k + m + g
     bstride = (B + a.pad + 255) // 256 * 256
     sstride = nblk * bstride
-    S = a.stripes
     buf = torch.empty(S * sstride, dtype=torch.uint8, device="cuda")
     out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
     stream = c_void_p(torch.cuda.current_stream().cuda_stream)
@@ -82,7 +88,7 @@ def main():
                 got = buf[(k) * bstride:(k) * bstride + B]
                 if not torch.equal(got, ref):
                     print(f"  !! {name}: parity differs from {libs[0][0]}")
-    print(f"CL(k={k},r={r},m={m}) B={a.mib} MiB x{S} stripes; GB/s median (min..max) over {a.rounds} rounds")
+    print(f"{a.code}(k={k},r={r},m={m}) B={B} x{S} stripes pad={a.pad}; GB/s median (min..max) over {a.rounds} rounds")
     for name, (en, rp) in res.items():
         print(f"{name:28s} encode {statistics.median(en):8.1f} ({min(en):7.1f}..{max(en):7.1f})   "
               f"repair {statistics.median(rp):8.1f} ({min(rp):7.1f}..{max(rp):7.1f})", flush=True)
