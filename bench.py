@@ -41,6 +41,9 @@ def parse():
     ap.add_argument("--cpu-sample-mib", type=float, default=4.0)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
     ap.add_argument("--verify", action="store_true", help="check one stripe against the oracle after timing")
+    ap.add_argument("--hbm-fill", action="store_true",
+                    help="BASELINE configs[3]: 256 stripes per GPU, block size = the largest whole MiB "
+                         "that fits the GPU's free HBM")
     ap.add_argument("--host-resident", action="store_true",
                     help="measure the PCIe-inclusive rate (pinned host blocks) instead")
     return ap.parse_args()
@@ -205,10 +208,18 @@ def main():
     import ecwide_amd as E
 
     k, m, r = args.k, args.m, args.r
+    S = args.stripes
+    if args.hbm_fill:
+        S = 256
+        free = torch.cuda.mem_get_info(local)[0]
+        g0 = -(-k // r)
+        # slab: S * (k+m+g) blocks of B + 4 KiB pad, plus the S-block repair output
+        per_mib = S * ((k + m + g0) * ((1 << 20) + 4096) + (1 << 20))
+        args.block_mib = float(int(0.97 * free) // per_mib)
+        assert args.block_mib >= 1, f"{free} B free: too small for {S} stripes"
     B = int(args.block_mib * (1 << 20))
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
     codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
-    S = args.stripes
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
     from ecwide_amd.shard import weak_shard
@@ -300,8 +311,9 @@ def main():
         "dtype": "u8",
         "data": "synthetic (counter PRNG, uniform random bytes, generated in HBM)",
         "config": {
-            "workload": f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S} stripes/GPU: batched encode + "
-                        f"repair of D0",
+            "workload": (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S} stripes/GPU: batched encode + "
+                         f"repair of D0") + (" [configs[3]: 256 stripes filling HBM, "
+                                             f"{slab.buf.numel() / 2**30:.1f} GiB slab]" if args.hbm_fill else ""),
             "k": k, "r": r, "m": m, "g": g, "block_bytes": B, "stripes_per_gpu": S,
             "parallelism": f"stripe-partitioned x{world} (no collectives on the data path)",
             "encode_bytes_per_step_per_gpu": enc_bytes,
