@@ -44,6 +44,9 @@ def parse():
     ap.add_argument("--hbm-fill", action="store_true",
                     help="BASELINE configs[3]: 256 stripes per GPU, block size = the largest whole MiB "
                          "that fits the GPU's free HBM")
+    ap.add_argument("--strong", action="store_true",
+                    help="strong scaling (BASELINE configs[4]): --stripes (or the --hbm-fill batch) is the "
+                         "TOTAL, split by stripe across the ranks")
     ap.add_argument("--host-resident", action="store_true",
                     help="measure the PCIe-inclusive rate (pinned host blocks) instead")
     return ap.parse_args()
@@ -218,13 +221,15 @@ def main():
         args.block_mib = float(int(0.97 * free) // per_mib)
         assert args.block_mib >= 1, f"{free} B free: too small for {S} stripes"
     B = int(args.block_mib * (1 << 20))
+    from ecwide_amd.shard import stripe_shard, weak_shard
+
+    S_total = S if args.strong else S * world
+    # each rank owns distinct stripe ids; no data exchange between ranks
+    s0, S = stripe_shard(S_total, world, rank) if args.strong else weak_shard(S, rank)
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
     codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
-    from ecwide_amd.shard import weak_shard
-
-    s0, _ = weak_shard(S, rank)  # each rank owns distinct stripe ids, no data exchange
     slab.fill_random(seed=args.seed, s0=s0)
     torch.cuda.synchronize()
     enc_bytes = slab.encode_bytes()
@@ -285,7 +290,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    total_bytes = step_bytes * world * args.steps
+    total_bytes = step_bytes // S * S_total * args.steps  # every stripe costs the same bytes
     value = total_bytes / el_max / 1e9
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
     traffic = None
@@ -306,15 +311,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(el_max / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.strong else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (counter PRNG, uniform random bytes, generated in HBM)",
         "config": {
             "workload": (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S} stripes/GPU: batched encode + "
-                         f"repair of D0") + (" [configs[3]: 256 stripes filling HBM, "
+                         f"repair of D0") + (f" [strong: {S_total} stripes in total]" if args.strong else "") + (" [configs[3]: 256 stripes filling HBM, "
                                              f"{slab.buf.numel() / 2**30:.1f} GiB slab]" if args.hbm_fill else ""),
-            "k": k, "r": r, "m": m, "g": g, "block_bytes": B, "stripes_per_gpu": S,
+            "k": k, "r": r, "m": m, "g": g, "block_bytes": B, "stripes_per_gpu": S, "stripes_total": S_total,
             "parallelism": f"stripe-partitioned x{world} (no collectives on the data path)",
             "encode_bytes_per_step_per_gpu": enc_bytes,
             "repair_bytes_per_step_per_gpu": rep_bytes,
