@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--rows", type=int, default=128)
     ap.add_argument("--lib", default=None)
+    ap.add_argument("--pads", default="0,4096,73728,1060864")
+    ap.add_argument("--ns", default="1,2,4,8,16,27,64,128")
+    ap.add_argument("--no-copy", action="store_true")
     a = ap.parse_args()
     import torch
 
@@ -45,16 +48,17 @@ def main():
     stream = c_void_p(torch.cuda.current_stream().cuda_stream)
     big = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
     dst = torch.empty(8 << 30, dtype=torch.uint8, device="cuda")
-    t = timeit(lambda: dst.copy_(big))
-    print(f"torch copy 8 GiB: {2 * big.numel() / t / 1e9:8.1f} GB/s")
+    if not a.no_copy:
+        t = timeit(lambda: dst.copy_(big))
+        print(f"torch copy 8 GiB: {2 * big.numel() / t / 1e9:8.1f} GB/s")
     del dst
     out = torch.empty(B, dtype=torch.uint8, device="cuda")
-    for pad in (0, 4096, 65536 + 4096, (1 << 20) + 12288):
+    for pad in [int(x) for x in a.pads.split(",")]:
         stride = B + pad
         nrows = min(a.rows, (big.numel() - B) // stride + 1)
         base = big.data_ptr()
         line = f"stride B+{pad:>8}: "
-        for n in (1, 2, 4, 8, 16, 27, 64, 128):
+        for n in [int(x) for x in a.ns.split(",")]:
             if n > nrows:
                 break
             arr = (c_void_p * n)(*[base + i * stride for i in range(n)])
