@@ -1,0 +1,309 @@
+// Hand-scheduled encode of ONE full column tile (gfx950 / CDNA4), used by
+// encode_kernel_slab for slab batches with <= 4 global rows per pass.
+//
+// Same arithmetic as encode_tile() in ecw_kernels.hip (ISA-L's 4-bit split
+// GF(2^8) products, gf_vect_mul_init, isal:erasure_code/ec_base.c:157-262,
+// with the tables of all rows of the pass packed into one LDS entry), but the
+// row loop is written out so that every wait is explicit:
+//
+//   * two-slot register ring: row j+2 is loaded into the slot row j is
+//     consumed from, and each consumption waits with vmcnt(1) -- exactly the
+//     one newer ring load may stay in flight. Local-parity stores issued in
+//     between do not break the count: loads return in order, so vmcnt(1)
+//     with extra stores outstanding can only wait longer, never too little.
+//     (Compiled from C++, any store in the row loop makes LLVM's waitcnt pass
+//     fall back to vmcnt(0) at the loop head, i.e. drain the ring every two
+//     rows; that cost ~4 % of encode time at k=128.)
+//   * per row: the 32 table lookups are issued in two alternating sets of 8
+//     (ds_read_b32 into the address register itself), each set folded into
+//     the packed accumulators with v_bitop3 (xor3) while the next is in
+//     flight (lgkmcnt(8));
+//   * local parities: XOR of the group's rows in v[28:31], stored with a
+//     global_store at the group's last row (all-zero in ECWide-C literal
+//     mode, still written);
+//   * global parities: v_perm byte transpose of the 16 packed accumulators,
+//     one dwordx4 store per output row.
+//
+// Fixed registers (all declared clobbered; 57 VGPRs, 78 when parking):
+//   v[4:7] ring slot A, v[8:11] ring slot B, v[12:27] packed accumulators
+//   (byte column c of the lane's 16 in v[12+c]), v[28:31] local parity,
+//   v32 table-record high byte, v33 nibble mask, v34/v35 nibble words,
+//   v[36:39] output row, v40 column offset, v[41:48] / v[49:56] lookup sets.
+//   s[40:41] next row to load, s[42:43] current local block, s44 row index,
+//   s45 end of the current group, s46 LDS table record of the row, s47/s48
+//   record high/low bytes, s49 scratch, s[50:53] v_perm selectors, s[54:55]
+//   global output row, s56 output index, s57/s58 transpose selectors,
+//   s59 finished groups; v[58:77] parked local parities (tuples start on
+//   even registers on gfx950).
+#pragma once
+
+
+// nibble words of data dword W (lo = (W<<2)&0x3C.. | rec.lo, hi = (W>>2)&..),
+// then the 8 lookup addresses (record.hi << 8 | nibble*4) into set A0..A7
+#define ECW_DW_ADDR(W, A0, A1, A2, A3, A4, A5, A6, A7) \
+  "v_lshlrev_b32 v34, 2, " W "\n\t"                    \
+  "v_lshrrev_b32 v35, 2, " W "\n\t"                    \
+  "v_and_or_b32 v34, v34, v33, s48\n\t"                \
+  "v_and_or_b32 v35, v35, v33, s48\n\t"                \
+  "v_perm_b32 " A0 ", v32, v34, s50\n\t"               \
+  "v_perm_b32 " A1 ", v32, v35, s50\n\t"               \
+  "v_perm_b32 " A2 ", v32, v34, s51\n\t"               \
+  "v_perm_b32 " A3 ", v32, v35, s51\n\t"               \
+  "v_perm_b32 " A4 ", v32, v34, s52\n\t"               \
+  "v_perm_b32 " A5 ", v32, v35, s52\n\t"               \
+  "v_perm_b32 " A6 ", v32, v34, s53\n\t"               \
+  "v_perm_b32 " A7 ", v32, v35, s53\n\t"
+
+// lo-nibble products at +0, hi-nibble products at +64 of the record
+#define ECW_DW_READ(A0, A1, A2, A3, A4, A5, A6, A7) \
+  "ds_read_b32 " A0 ", " A0 "\n\t"                   \
+  "ds_read_b32 " A1 ", " A1 " offset:64\n\t"         \
+  "ds_read_b32 " A2 ", " A2 "\n\t"                   \
+  "ds_read_b32 " A3 ", " A3 " offset:64\n\t"         \
+  "ds_read_b32 " A4 ", " A4 "\n\t"                   \
+  "ds_read_b32 " A5 ", " A5 " offset:64\n\t"         \
+  "ds_read_b32 " A6 ", " A6 "\n\t"                   \
+  "ds_read_b32 " A7 ", " A7 " offset:64\n\t"
+
+#define ECW_DW_FOLD(C0, C1, C2, C3, A0, A1, A2, A3, A4, A5, A6, A7) \
+  "v_bitop3_b32 " C0 ", " C0 ", " A0 ", " A1 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " C1 ", " C1 ", " A2 ", " A3 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " C2 ", " C2 ", " A4 ", " A5 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " C3 ", " C3 ", " A6 ", " A7 " bitop3:0x96\n\t"
+
+#define ECW_ADDR_X(W) ECW_DW_ADDR(W, "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48")
+#define ECW_ADDR_Y(W) ECW_DW_ADDR(W, "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56")
+#define ECW_READ_X ECW_DW_READ("v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48")
+#define ECW_READ_Y ECW_DW_READ("v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56")
+#define ECW_FOLD_X(C0, C1, C2, C3) ECW_DW_FOLD(C0, C1, C2, C3, "v41", "v42", "v43", "v44", "v45", "v46", "v47", "v48")
+#define ECW_FOLD_Y(C0, C1, C2, C3) ECW_DW_FOLD(C0, C1, C2, C3, "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56")
+
+// One data row from ring slot R0..R3 (s46 = its LDS table record): GF
+// products into the accumulators, XOR into the local parity (XL = 1).
+#define ECW_ROW(R0, R1, R2, R3, XL)                                   \
+  "s_lshr_b32 s47, s46, 8\n\t"                                        \
+  "s_and_b32 s48, s46, 0xff\n\t"                                      \
+  "s_mul_i32 s48, s48, 0x01010101\n\t"                                \
+  "v_mov_b32 v32, s47\n\t"                                            \
+  ECW_ADDR_X(R0) ECW_READ_X                                           \
+  ECW_ADDR_Y(R1) ECW_READ_Y                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_X("v12", "v13", "v14", "v15")                              \
+  ECW_ADDR_X(R2) ECW_READ_X                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_Y("v16", "v17", "v18", "v19")                              \
+  ECW_ADDR_Y(R3) ECW_READ_Y                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_X("v20", "v21", "v22", "v23")                              \
+  ECW_LACC_##XL(R0, R1, R2, R3)                                       \
+  "s_waitcnt lgkmcnt(0)\n\t"                                          \
+  ECW_FOLD_Y("v24", "v25", "v26", "v27")                              \
+  "s_add_u32 s46, s46, 128\n\t"
+
+#define ECW_LACC_0(R0, R1, R2, R3)
+#define ECW_LACC_1(R0, R1, R2, R3)     \
+  "v_xor_b32 v28, v28, " R0 "\n\t"     \
+  "v_xor_b32 v29, v29, " R1 "\n\t"     \
+  "v_xor_b32 v30, v30, " R2 "\n\t"     \
+  "v_xor_b32 v31, v31, " R3 "\n\t"
+
+// End of the local group at row s44 (0-based)? Store the local parity,
+// advance to the next local block and group. ZL = 1: reset the XOR.
+#define ECW_BOUNDARY_NONE
+#define ECW_BOUNDARY(ZL)                                  \
+  "s_add_u32 s49, s44, 1\n\t"                             \
+  "s_cmp_eq_u32 s49, s45\n\t"                             \
+  "s_cbranch_scc0 20f\n\t"                                \
+  ECW_ASM_LSTORE                                          \
+  "s_add_u32 s42, s42, %[bslo]\n\t"                       \
+  "s_addc_u32 s43, s43, %[bshi]\n\t"                      \
+  "s_add_u32 s45, s45, %[r]\n\t"                          \
+  "s_min_u32 s45, s45, %[k]\n\t"                          \
+  "s_nop 1\n\t"                                           \
+  ECW_LRESET_##ZL                                         \
+  "20:\n\t"
+// Parked variant (<= 5 groups): the finished local parity is copied into
+// v[58+4t:61+4t] and all locals are stored at the end of the tile, next to
+// the global rows. Mid-tile stores measured ~9 % of encode time at k=128
+// (3.7 % of the bytes): writes scattered between the row reads cost the
+// DRAM far more than the same writes issued together.
+#define ECW_PARK(T, V0, V1, V2, V3, NEXT)                                   \
+  "s_cmp_eq_u32 s59, " #T "\n\t"                                            \
+  "s_cbranch_scc0 " #NEXT "f\n\t"                                           \
+  "v_mov_b32 " V0 ", v28\n\tv_mov_b32 " V1 ", v29\n\t"                       \
+  "v_mov_b32 " V2 ", v30\n\tv_mov_b32 " V3 ", v31\n\t"                       \
+  "s_branch 26f\n\t" #NEXT ":\n\t"
+#define ECW_BOUNDARY_PARK                                   \
+  "s_add_u32 s49, s44, 1\n\t"                               \
+  "s_cmp_eq_u32 s49, s45\n\t"                               \
+  "s_cbranch_scc0 20f\n\t"                                  \
+  ECW_PARK(0, "v58", "v59", "v60", "v61", 21)               \
+  ECW_PARK(1, "v62", "v63", "v64", "v65", 22)               \
+  ECW_PARK(2, "v66", "v67", "v68", "v69", 23)               \
+  ECW_PARK(3, "v70", "v71", "v72", "v73", 24)               \
+  ECW_PARK(4, "v74", "v75", "v76", "v77", 25)               \
+  "26:\n\t"                                                 \
+  "s_add_u32 s59, s59, 1\n\t"                               \
+  "s_add_u32 s45, s45, %[r]\n\t"                            \
+  "s_min_u32 s45, s45, %[k]\n\t"                            \
+  ECW_LRESET_1                                              \
+  "20:\n\t"
+// store parked local t (if t < number of groups) and advance the block
+#define ECW_UNPARK(T, V)                                                    \
+  "s_cmp_le_u32 s59, " #T "\n\t"                                            \
+  "s_cbranch_scc1 27f\n\t"                                                  \
+  "global_store_dwordx4 v40, " V ", s[42:43]" ECW_ASM_STMOD "\n\t"          \
+  "s_add_u32 s42, s42, %[bslo]\n\t"                                         \
+  "s_addc_u32 s43, s43, %[bshi]\n\t"
+#define ECW_STORE_PARKED                                                    \
+  "s_mov_b64 s[42:43], %[lrow0]\n\t"                                        \
+  ECW_UNPARK(0, "v[58:61]") ECW_UNPARK(1, "v[62:65]") ECW_UNPARK(2, "v[66:69]") \
+  ECW_UNPARK(3, "v[70:73]") ECW_UNPARK(4, "v[74:77]")                       \
+  "27:\n\t"
+#define ECW_LRESET_0
+#define ECW_LRESET_1 "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t"
+
+#ifndef ECW_ASM_DIAG_NOLSTORE
+#define ECW_ASM_LSTORE "global_store_dwordx4 v40, v[28:31], s[42:43]" ECW_ASM_STMOD "\n\t"
+#else
+#define ECW_ASM_LSTORE  // diagnostic builds only: time the encode without its local-parity stores
+#endif
+#ifndef ECW_ASM_STMOD
+#define ECW_ASM_STMOD " nt"  // parity stores: nontemporal (+3 % encode, measured)
+#endif
+#ifndef ECW_ASM_LDMOD
+#define ECW_ASM_LDMOD " nt"  // ring loads: nontemporal, every byte is read once (+2 %, measured)
+#endif
+#define ECW_LOAD_A "global_load_dwordx4 v[4:7], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
+#define ECW_LOAD_B "global_load_dwordx4 v[8:11], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
+#define ECW_NEXTROW "s_add_u32 s40, s40, %[bslo]\n\ts_addc_u32 s41, s41, %[bshi]\n\t"
+#define ECW_ROW_A(XL) ECW_ROW("v4", "v5", "v6", "v7", XL)
+#define ECW_ROW_B(XL) ECW_ROW("v8", "v9", "v10", "v11", XL)
+
+// The whole tile. BND is the boundary code (ECW_BOUNDARY(ZL) or nothing),
+// XL whether rows are XOR-ed into the local parity.
+#define ECW_TILE_ASM(BND, XL, END)                                             \
+  "v_mov_b32 v40, %[col]\n\t"                                               \
+  "v_mov_b32 v33, 0x3c3c3c3c\n\t"                                           \
+  "s_mov_b32 s50, 0x0c0c0400\n\t"                                           \
+  "s_mov_b32 s51, 0x0c0c0401\n\t"                                           \
+  "s_mov_b32 s52, 0x0c0c0402\n\t"                                           \
+  "s_mov_b32 s53, 0x0c0c0403\n\t"                                           \
+  "s_mov_b64 s[40:41], %[row0]\n\t"                                         \
+  ECW_LOAD_A ECW_NEXTROW ECW_LOAD_B ECW_NEXTROW                             \
+  "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
+  "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
+  "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
+  "v_mov_b32 v24, 0\n\tv_mov_b32 v25, 0\n\tv_mov_b32 v26, 0\n\tv_mov_b32 v27, 0\n\t" \
+  "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  "s_mov_b32 s44, 0\n\t"                                                    \
+  "s_mov_b32 s59, 0\n\t"                                                    \
+  "s_mov_b32 s46, %[lds]\n\t"                                               \
+  "s_mov_b64 s[42:43], %[lrow0]\n\t"                                        \
+  "s_min_u32 s45, %[r], %[k]\n\t"                                           \
+  /* main loop: rows j, j+1 while rows j+2, j+3 exist */                    \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 3\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW                                  \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW                                  \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  /* 2 or 3 rows left (k - j); slot A holds row j, slot B row j+1 */        \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc0 12f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_A(XL) BND ECW_LOAD_A                                              \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_B(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW_ROW_A(XL) BND                                                         \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_A(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW_ROW_B(XL) BND                                                         \
+  "13:\n\t"                                                                 \
+  END                                                                       \
+  /* global rows: byte l of the packed accumulators -> output row l */      \
+  "s_mov_b64 s[54:55], %[grow0]\n\t"                                        \
+  "s_mov_b32 s56, 0\n\t"                                                    \
+  "30:\n\t"                                                                 \
+  "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
+  "s_cbranch_scc1 31f\n\t"                                                  \
+  "s_add_u32 s49, s56, 4\n\t"                                               \
+  "s_lshl_b32 s57, s49, 8\n\t"                                              \
+  "s_or_b32 s57, s57, s56\n\t"                                              \
+  "s_or_b32 s57, s57, 0x0c0c0000\n\t"                                       \
+  "s_lshl_b32 s58, s49, 24\n\t"                                             \
+  "s_lshl_b32 s49, s56, 16\n\t"                                             \
+  "s_or_b32 s58, s58, s49\n\t"                                              \
+  "s_or_b32 s58, s58, 0x0c0c\n\t"                                           \
+  "v_perm_b32 v34, v13, v12, s57\n\t"                                       \
+  "v_perm_b32 v35, v15, v14, s58\n\t"                                       \
+  "v_or_b32 v36, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, v17, v16, s57\n\t"                                       \
+  "v_perm_b32 v35, v19, v18, s58\n\t"                                       \
+  "v_or_b32 v37, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, v21, v20, s57\n\t"                                       \
+  "v_perm_b32 v35, v23, v22, s58\n\t"                                       \
+  "v_or_b32 v38, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, v25, v24, s57\n\t"                                       \
+  "v_perm_b32 v35, v27, v26, s58\n\t"                                       \
+  "v_or_b32 v39, v34, v35\n\t"                                              \
+  "global_store_dwordx4 v40, v[36:39], s[54:55]" ECW_ASM_STMOD "\n\t"      \
+  "s_nop 1\n\t"                                                             \
+  "s_add_u32 s54, s54, %[bslo]\n\t"                                         \
+  "s_addc_u32 s55, s55, %[bshi]\n\t"                                        \
+  "s_add_u32 s56, s56, 1\n\t"                                               \
+  "s_branch 30b\n\t"                                                        \
+  "31:"
+
+#define ECW_TILE_OPERANDS                                                          \
+  : : [row0] "s"(row0), [lrow0] "s"(lrow0), [grow0] "s"(grow0), [bslo] "s"(bslo), \
+    [bshi] "s"(bshi), [k] "s"(k), [r] "s"(r), [nrows] "s"(nrows), [lds] "s"(lds), \
+    [col] "v"(col)                                                                 \
+  : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18",  \
+    "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32",  \
+    "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46",  \
+    "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "s40", "s41", "s42", "s43", \
+    "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57",  \
+    "s58", "s59", "scc", "memory"
+
+#define ECW_TILE_OPERANDS_PARK                                                     \
+  ECW_TILE_OPERANDS, "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", \
+    "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77"
+
+namespace ecw {
+namespace {
+
+// LOCAL: kLocalNone / kLocalXor / kLocalZero (ecw_internal.hpp); PARK: keep
+// the (<= 5) local parities in registers until the end of the tile. Requires
+// k >= 2, a full tile (every lane's 16 bytes in range) and exec = all lanes.
+template <int LOCAL, bool PARK>
+__device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
+                                                int k, int r, int nrows, uint32_t lds, uint32_t col) {
+  const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
+  if constexpr (LOCAL == kLocalNone) {
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_NONE, 0, ) ECW_TILE_OPERANDS);
+  } else if constexpr (LOCAL == kLocalXor && PARK) {
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_PARK, 1, ECW_STORE_PARKED) ECW_TILE_OPERANDS_PARK);
+  } else if constexpr (LOCAL == kLocalXor) {
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(1), 1, ) ECW_TILE_OPERANDS);
+  } else {
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(0), 0, ) ECW_TILE_OPERANDS);
+  }
+}
+
+}  // namespace
+}  // namespace ecw

@@ -27,9 +27,16 @@
 #include <type_traits>
 
 #include "ecw_internal.hpp"
+#include "ecw_encode_asm.hpp"
 
 namespace ecw {
 namespace {
+
+#ifndef ECW_ASM_PARK
+#define ECW_ASM_PARK 1  // <= 5 local parities: store them at the end of the tile
+#endif
+constexpr int kPrefetchEncAsmTail = 2;
+constexpr int kMaxParkedLocals = ECW_ASM_PARK ? 5 : 0;  // v[58:77] of the asm tile
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -350,6 +357,51 @@ __global__ __launch_bounds__(kBlock, ECW_ENC_MIN_WAVES) void encode_kernel(const
   }
 }
 
+#ifndef ECW_ENC_ASM
+#define ECW_ENC_ASM 1  // slab batches with <= 4 global rows: hand-scheduled tile loop (ecw_encode_asm.hpp)
+#endif
+#ifndef ECW_ASM_MIN_WAVES
+#define ECW_ASM_MIN_WAVES 6  // 80 VGPRs: the parked asm tile uses 77 (6 measured >= 8 also without parking)
+#endif
+
+__device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
+  const uint64_t v = reinterpret_cast<uint64_t>(p);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+}
+
+// Slab encode with <= 4 global rows (one u32 table entry per nibble) and
+// k >= 2: full tiles through the hand-scheduled asm tile, the ragged last
+// tile of a block through encode_tile<..., TAIL>. PARK (<= 5 groups): local
+// parities are stored at the end of each tile (ecw_encode_asm.hpp).
+template <int LOCAL, bool PARK>
+__global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_slab(const SlabRows rows, const EncodeGeom g,
+                                                                               const uint4* __restrict__ tbl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int n16 = g.k * 8;
+  for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
+  __syncthreads();
+  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  const int k = __builtin_amdgcn_readfirstlane(g.k);
+  const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
+  const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
+  const uint64_t bs = rows.bstride;
+  for (uint64_t tile = g.tile_begin + blockIdx.x; tile < g.tile_end; tile += gridDim.x) {
+    const TileAt cur = tile_at(g, tile);
+    if (cur.full) {
+      const uint8_t* sb = uniform_ptr(rows.base + static_cast<uint64_t>(cur.s) * rows.sstride);
+      encode_tile_asm<LOCAL, PARK>(sb, const_cast<uint8_t*>(sb + static_cast<uint64_t>(k + g.m) * bs),
+                             const_cast<uint8_t*>(sb + static_cast<uint64_t>(k + g.row0) * bs), bs, k, r, nrows,
+                             __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+    } else {
+      uint4 ring[kPrefetchEncAsmTail];
+      ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
+      encode_tile<1, kPrefetchEncAsmTail, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
+    }
+  }
+}
+
 // ---- XOR reduce: dst = src_0 ^ ... ^ src_{n-1} ----------------------------
 __device__ __forceinline__ const uint8_t* xsrc(const XorPtr& a, int, int i) { return a.src[i]; }
 __device__ __forceinline__ const uint8_t* xsrc(const XorSlab& a, int s, int i) {
@@ -468,6 +520,24 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
   return hipGetLastError();
 }
 
+hipError_t launch_encode_slab_asm(const SlabRows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(g.k) * 128;
+  switch (g.local_mode) {
+    case kLocalXor:
+      if (g.groups <= kMaxParkedLocals)
+        hipLaunchKernelGGL((encode_kernel_slab<kLocalXor, true>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      else
+        hipLaunchKernelGGL((encode_kernel_slab<kLocalXor, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    case kLocalZero:
+      hipLaunchKernelGGL((encode_kernel_slab<kLocalZero, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    default:
+      hipLaunchKernelGGL((encode_kernel_slab<kLocalNone, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+  }
+  return hipGetLastError();
+}
+
 #ifndef ECW_COHORT_TILES
 #define ECW_COHORT_TILES 0  // > 0: launch the slab in windows of this many tiles (tuning)
 #endif
@@ -484,8 +554,15 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
     g.tile_begin = t0;
     g.tile_end = t0 + win < total ? t0 + win : total;
     const dim3 grid(grid_for(g.tile_end - g.tile_begin));
-    const hipError_t e =
-        g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
+    hipError_t e;
+    if constexpr (std::is_same<Rows, SlabRows>::value) {
+      if (ECW_ENC_ASM && g.nrows <= 4 && g.k >= 2) {
+        e = launch_encode_slab_asm(rows, g, tbl, grid, s);
+        if (e != hipSuccess) return e;
+        continue;
+      }
+    }
+    e = g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
