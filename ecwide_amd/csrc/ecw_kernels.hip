@@ -66,8 +66,15 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 #define ECW_BUFLOAD 1
 #endif
 
-template <bool TAIL>
+// NT: plain nontemporal load (the XOR reduce: a straight stream, measured
+// +4 % over the volatile buffer load the encode ring needs).
+template <bool TAIL, bool NT = false>
 __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
+  if (NT && (!TAIL || col + 16 <= len)) {
+    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + col));
+    return make_uint4(v.x, v.y, v.z, v.w);
+  }
 #if ECW_BUFLOAD
   // Full tiles: a raw buffer load with the compiler-level volatile bit (aux
   // bit 31). Without it LLVM sinks the ring's prefetch loads down to their
@@ -103,16 +110,16 @@ __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t
   return make_uint4(w[0], w[1], w[2], w[3]);
 }
 
-template <bool TAIL>
+template <bool TAIL, bool NT = false>
 __device__ __forceinline__ void st16(uint8_t* row, uint32_t col, uint32_t len, uint4 v) {
   if (!TAIL || col + 16 <= len) {
-#if ECW_NT_STORES
-    typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 w = {v.x, v.y, v.z, v.w};
-    __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(row + col));
-#else
-    *reinterpret_cast<uint4*>(row + col) = v;
-#endif
+    if (NT || ECW_NT_STORES) {
+      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      const u32x4 w = {v.x, v.y, v.z, v.w};
+      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(row + col));
+    } else {
+      *reinterpret_cast<uint4*>(row + col) = v;
+    }
     return;
   }
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
@@ -417,17 +424,17 @@ __device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s,
   const int n = g.n;
   uint4 ring[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL>(xsrc(a, s, p < n ? p : n - 1), col, len);
+  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL, true>(xsrc(a, s, p < n ? p : n - 1), col, len);
   uint4 acc = make_uint4(0, 0, 0, 0);
   for (int i0 = 0; i0 < n; i0 += P) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       const int i = i0 + p;
       if (i < n) acc = xor4(acc, ring[p]);
-      ring[p] = ld16<TAIL>(xsrc(a, s, i + P < n ? i + P : n - 1), col, len);
+      ring[p] = ld16<TAIL, true>(xsrc(a, s, i + P < n ? i + P : n - 1), col, len);
     }
   }
-  st16<TAIL>(xdst(a, s), col, len, acc);
+  st16<TAIL, true>(xdst(a, s), col, len, acc);
 }
 
 template <int P, class Args>
@@ -489,7 +496,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
 #define ECW_PREFETCH_XOR 8
 #endif
 #ifndef ECW_GRID_PER_CU
-#define ECW_GRID_PER_CU 64  // encode: workgroups per CU before tiles are grid-strided
+#define ECW_GRID_PER_CU 256  // encode: workgroups per CU before tiles are grid-strided (256 vs 64: +2.7 %)
 #endif
 #ifndef ECW_GRID_PER_CU_XOR
 #define ECW_GRID_PER_CU_XOR 512  // XOR reduce: one workgroup per tile (measured +7.7 %)
