@@ -58,6 +58,9 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 #ifndef ECW_NT_LOADS
 #define ECW_NT_LOADS 0
 #endif
+#ifndef ECW_XOR_NT
+#define ECW_XOR_NT 1  // XOR reduce: nontemporal loads and stores
+#endif
 #ifndef ECW_ABLATE
 #define ECW_ABLATE 0  // tuning builds only: 1 = skip the GF lookups, 2 = skip the data loads
 #endif
@@ -424,17 +427,17 @@ __device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s,
   const int n = g.n;
   uint4 ring[P];
 #pragma unroll
-  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL, true>(xsrc(a, s, p < n ? p : n - 1), col, len);
+  for (int p = 0; p < P; ++p) ring[p] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, p < n ? p : n - 1), col, len);
   uint4 acc = make_uint4(0, 0, 0, 0);
   for (int i0 = 0; i0 < n; i0 += P) {
 #pragma unroll
     for (int p = 0; p < P; ++p) {
       const int i = i0 + p;
       if (i < n) acc = xor4(acc, ring[p]);
-      ring[p] = ld16<TAIL, true>(xsrc(a, s, i + P < n ? i + P : n - 1), col, len);
+      ring[p] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, i + P < n ? i + P : n - 1), col, len);
     }
   }
-  st16<TAIL, true>(xdst(a, s), col, len, acc);
+  st16<TAIL, ECW_XOR_NT>(xdst(a, s), col, len, acc);
 }
 
 template <int P, class Args>
