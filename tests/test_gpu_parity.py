@@ -164,7 +164,11 @@ def test_fill_kernel_matches_oracle(E, torch, orc):
 
 @pytest.mark.parametrize("k,m,r,B,S", [(32, 3, 11, 1 << 20, 2), (32, 2, 8, (1 << 18) + 48, 3),
                                        (128, 3, 27, 1 << 18, 2), (20, 8, 6, 70000, 2), (40, 11, 9, 12345, 2),
-                                       (5, 5, 2, 4096, 4), (250, 6, 50, 8192, 1), (7, 1, 7, 16, 5)])
+                                       (5, 5, 2, 4096, 4), (250, 6, 50, 8192, 1), (7, 1, 7, 16, 5),
+                                       # asm tile (slab, <= 4 global rows): odd k (3-row epilogue), the
+                                       # minimum k = 2, one group, > 5 groups (stores not parked)
+                                       (33, 3, 4, 3 * 4096 + 100, 2), (31, 4, 31, 8192, 2), (2, 1, 1, 8192, 3),
+                                       (3, 2, 2, 8192, 2), (128, 3, 8, 1 << 16, 2), (6, 4, 1, 4096, 2)])
 def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S):
     """Batched slab encode vs oracle at mid sizes; repair of every data and
     local block of stripe 0 equals the erased block."""
@@ -245,15 +249,24 @@ def test_multinode_encode_chain(E, torch, orc, k, m, r, B):
         assert np.array_equal(chain[i].cpu().numpy(), want[i]), i
 
 
-def test_literal_mode_slab_writes_zero_locals(E, torch):
-    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(32, 2, 8, 65536), 1, False, local_mode="literal")
-    slab = E.StripeSlab(c, stripes=2, block_bytes=65536)
+@pytest.mark.parametrize("k,m,r", [(32, 2, 8), (33, 3, 4)])
+def test_literal_mode_slab_writes_zero_locals(E, torch, orc, k, m, r):
+    """ECWide-C literal mode: every L block is written as zeros (parked and
+    unparked asm paths); the global parities are unchanged."""
+    B = 65536 + 100
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode="literal")
+    slab = E.StripeSlab(c, stripes=2, block_bytes=B)
     slab.buf.fill_(0x5A)
     slab.fill_random(seed=3)
     slab.encode()
     torch.cuda.synchronize()
+    oc = orc.codec("C", k, m, r, B)
     for st in range(2):
-        for L in slab.parity(st)[2:]:
+        want = oc.encode([orc.fill(B, 3, st, j) for j in range(k)], threads=8)
+        par = slab.parity(st)
+        for i in range(m):
+            assert np.array_equal(par[i].cpu().numpy(), want[i]), (st, i)
+        for L in par[m:]:
             assert not L.any()
 
 
