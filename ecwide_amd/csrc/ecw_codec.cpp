@@ -134,8 +134,27 @@ struct EncodeTarget {
   int stripes = 1;
 };
 
-int run_encode(ecw_codec* c, const EncodeTarget& t, size_t len, hipStream_t s) {
+// Pointer-mode rows that are really a strided layout (data blocks at one
+// stride, parity blocks -- globals then locals -- at the same stride, e.g. two
+// [k, B] / [m+g, B] tensors): describe them as a one-stripe slab, so the
+// encode takes the slab kernel (asm tile) instead of the pointer kernel.
+bool as_slab(const uint8_t* const* src, int k, uint8_t* const* dst, int np, SlabRows* out) {
+  auto at = [](const void* p) { return static_cast<uint64_t>(reinterpret_cast<uintptr_t>(p)); };
+  if (k < 2 || np < 1 || at(src[1]) <= at(src[0])) return false;
+  const uint64_t bs = at(src[1]) - at(src[0]);
+  for (int j = 2; j < k; ++j)
+    if (at(src[j]) != at(src[0]) + j * bs) return false;
+  for (int i = 1; i < np; ++i)
+    if (at(dst[i]) != at(dst[0]) + i * bs) return false;
+  *out = SlabRows{src[0], bs, 0, dst[0]};
+  return true;
+}
+
+int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) {
   const int k = c->k(), m = c->m(), ng = c->groups();
+  EncodeTarget t = t0;
+  SlabRows strided;
+  if (!t.slab && t.stripes == 1 && as_slab(t.src, k, t.dst, c->info.parity_num, &strided)) t.slab = &strided;
   const int lmode = local_mode_of(c);
   if (len == 0 || t.stripes == 0) return ECW_OK;
   EncodeGeom g{};
@@ -179,7 +198,7 @@ int run_encode(ecw_codec* c, const EncodeTarget& t, size_t len, hipStream_t s) {
         xs.base = t.slab->base;
         xs.bstride = t.slab->bstride;
         xs.sstride = t.slab->sstride;
-        xs.out = const_cast<uint8_t*>(t.slab->base) + static_cast<uint64_t>(k + m + i) * t.slab->bstride;
+        xs.out = t.slab->pbase + static_cast<uint64_t>(m + i) * t.slab->bstride;
         xs.ostride = t.slab->sstride;
         for (int u = 0; u < n; ++u) xs.idx[u] = j0 + u;
         if (lmode == kLocalZero) {
@@ -558,7 +577,7 @@ int ecw_encode_batch_dev(ecw_codec* c, uint8_t* d_slab, size_t block_stride, siz
   }
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
-  SlabRows slab{d_slab, block_stride, stripe_stride};
+  const SlabRows slab = slab_rows(d_slab, block_stride, stripe_stride, c->k());
   EncodeTarget t;
   t.slab = &slab;
   t.stripes = stripes;
@@ -789,7 +808,7 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
             return ECW_EDEVICE;
       if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return ECW_EDEVICE;
       if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return ECW_EDEVICE;
-      SlabRows slab{base, cstride, stripe_bytes};
+      const SlabRows slab = slab_rows(base, cstride, stripe_bytes, k);
       EncodeTarget t;
       t.slab = &slab;
       t.stripes = ns;

@@ -142,15 +142,13 @@ __device__ __forceinline__ uint8_t* glob_row(const PtrRows& r, const EncodeGeom&
   return r.dst[l];
 }
 __device__ __forceinline__ uint8_t* glob_row(const SlabRows& r, const EncodeGeom& g, int s, int l) {
-  return const_cast<uint8_t*>(r.base) + s * r.sstride +
-         static_cast<uint64_t>(g.k + g.row0 + l) * r.bstride;
+  return r.pbase + s * r.sstride + static_cast<uint64_t>(g.row0 + l) * r.bstride;
 }
 __device__ __forceinline__ uint8_t* local_row(const PtrRows& r, const EncodeGeom& g, int, int t) {
   return r.dst[g.nrows + t];
 }
 __device__ __forceinline__ uint8_t* local_row(const SlabRows& r, const EncodeGeom& g, int s, int t) {
-  return const_cast<uint8_t*>(r.base) + s * r.sstride +
-         static_cast<uint64_t>(g.k + g.m + t) * r.bstride;
+  return r.pbase + s * r.sstride + static_cast<uint64_t>(g.m + t) * r.bstride;
 }
 
 // ---- GF(2^8) multiply-accumulate of one 16-byte row slice -----------------
@@ -229,20 +227,6 @@ __device__ __forceinline__ void ring_prologue(uint4 (&ring)[P], const Rows& rows
     ring[p] = ld16<TAIL>(src_row(rows, g, t.s, p < g.k ? p : g.k - 1), t.col, static_cast<uint32_t>(g.len));
 }
 
-#ifndef ECW_LOCAL_LDS
-#define ECW_LOCAL_LDS 0
-#endif
-constexpr int kMaxLdsLocals = 8;  // local parities staged in LDS per tile (4 KiB each)
-
-// Local parities are staged in LDS (after the tables) when the launch has
-// few enough groups; the host sizes the dynamic LDS with the same rule.
-__host__ __device__ __forceinline__ bool stage_locals(const EncodeGeom& g) {
-  return ECW_LOCAL_LDS && g.local_mode != kLocalNone && g.groups <= kMaxLdsLocals;
-}
-__device__ __forceinline__ uint32_t loc_base(const EncodeGeom& g, uint32_t lds_base) {
-  return lds_base + static_cast<uint32_t>(g.k) * 128u * (g.nrows <= 4 ? 1u : 2u);
-}
-
 // One column tile: consumes the ring (rows 0..P-1 of `cur` already in flight)
 // and streams rows P..k-1 through it. In the last round of the row loop the
 // slots are refilled with rows 0..P-1 of the next tile when `pf`, so tiles
@@ -277,19 +261,9 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
         if constexpr (LOCAL != kLocalNone) {
           lacc = xor4(lacc, ring[p]);
           if (j + 1 == gend) {
-            const uint4 v = LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0);
-            if (!TAIL && stage_locals(g)) {
-              // park the finished local parity in LDS; the global store is
-              // issued with the global parities at the end of the tile (a
-              // store here would sit in vmcnt ahead of the next row's loads)
-              typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-              typedef __attribute__((address_space(3))) u32x4 lds_u32x4;
-              const u32x4 w = {v.x, v.y, v.z, v.w};
-              *reinterpret_cast<lds_u32x4*>(static_cast<uintptr_t>(
-                  loc_base(g, lds_base) + t * kTileBytes + threadIdx.x * kLaneBytes)) = w;
-            } else {
-              st16<TAIL>(local_row(rows, g, cur.s, t), col, len, v);
-            }
+            // (this store makes LLVM put vmcnt(0) at the loop head; the slab
+            // path avoids that with the asm tile, ecw_encode_asm.hpp)
+            st16<TAIL>(local_row(rows, g, cur.s, t), col, len, LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0));
             lacc = make_uint4(0, 0, 0, 0);
             ++t;
             gend = gend + g.r < k ? gend + g.r : k;
@@ -306,17 +280,6 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
     }
   }
   for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
-  if constexpr (LOCAL != kLocalNone) {
-    if (!TAIL && stage_locals(g)) {
-      typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-      typedef __attribute__((address_space(3))) const u32x4 lds_cu32x4;
-      for (int u = 0; u < g.groups; ++u) {
-        const u32x4 w = *reinterpret_cast<lds_cu32x4*>(static_cast<uintptr_t>(
-            loc_base(g, lds_base) + u * kTileBytes + threadIdx.x * kLaneBytes));
-        st16<false>(local_row(rows, g, cur.s, u), col, len, make_uint4(w.x, w.y, w.z, w.w));
-      }
-    }
-  }
 }
 
 template <int NW, int P, int LOCAL, class Rows>
@@ -400,10 +363,12 @@ __global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_slab(
   for (uint64_t tile = g.tile_begin + blockIdx.x; tile < g.tile_end; tile += gridDim.x) {
     const TileAt cur = tile_at(g, tile);
     if (cur.full) {
-      const uint8_t* sb = uniform_ptr(rows.base + static_cast<uint64_t>(cur.s) * rows.sstride);
-      encode_tile_asm<LOCAL, PARK>(sb, const_cast<uint8_t*>(sb + static_cast<uint64_t>(k + g.m) * bs),
-                             const_cast<uint8_t*>(sb + static_cast<uint64_t>(k + g.row0) * bs), bs, k, r, nrows,
-                             __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+      const uint64_t so = static_cast<uint64_t>(cur.s) * rows.sstride;
+      const uint8_t* sb = uniform_ptr(rows.base + so);
+      const uint8_t* pb = uniform_ptr(rows.pbase + so);
+      encode_tile_asm<LOCAL, PARK>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
+                                   const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * bs), bs, k, r, nrows,
+                                   __builtin_amdgcn_readfirstlane(lds_base), cur.col);
     } else {
       uint4 ring[kPrefetchEncAsmTail];
       ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
@@ -516,7 +481,7 @@ unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
 
 template <int NW, class Rows>
 hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
-  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + (stage_locals(g) ? size_t(g.groups) * kTileBytes : 0);
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
   switch (g.local_mode) {
     case kLocalXor:
       hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);

@@ -89,6 +89,36 @@ def test_encode_device_api_golden(E, torch, orc, manifest):
             assert np.array_equal(g.cpu().numpy(), w), (e["name"], i)
 
 
+@pytest.mark.parametrize("layout", ["strided", "reversed"])
+def test_encode_device_api_layouts(E, torch, orc, layout):
+    """ecw_encode_dev with every block in one buffer: at one stride (taken as a
+    one-stripe slab -> the asm tile) and in reverse order (pointer kernel);
+    both against the oracle, at shapes with full tiles and a ragged tail."""
+    for k, m, r, B in [(32, 3, 11, 3 * 4096 + 48), (128, 3, 27, 1 << 16), (9, 2, 3, 8192)]:
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+        np_ = c.parityNum
+        stride = (B + 255) // 256 * 256 + 4096
+        dbuf = torch.zeros((k, stride), dtype=torch.uint8, device="cuda")
+        pbuf = torch.full((np_, stride), 0x5A, dtype=torch.uint8, device="cuda")
+        data = [orc.fill(B, 17, 0, j) for j in range(k)]
+        for j in range(k):
+            dbuf[j, :B].copy_(torch.from_numpy(data[j]))
+        drows = [dbuf[j, :B] for j in range(k)]
+        prows = [pbuf[i, :B] for i in range(np_)]
+        if layout == "reversed":
+            order = list(range(k))[::-1]
+            for j in range(k):
+                dbuf[order[j], :B].copy_(torch.from_numpy(data[j]))
+            drows = [dbuf[order[j], :B] for j in range(k)]
+            prows = prows[::-1]
+        c.encodeData(drows, prows)
+        torch.cuda.synchronize()
+        want = orc.codec("C", k, m, r, B).encode(data, threads=8)
+        for i in range(np_):
+            assert np.array_equal(prows[i].cpu().numpy(), want[i]), (layout, k, i)
+        assert not pbuf[:, B:].ne(0x5A).any(), "wrote past the block"
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]
