@@ -334,6 +334,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            # PMC-measured HBM bytes of one launch over this run's launch time
+            "traffic_GBps": round(traffic / (enc_ms * 1e-3) / 1e9, 2) if traffic else None,
             "launch_ms": round(enc_ms, 4),
             "repair_launch_ms": round(rep_ms, 4),
             "repair_frac": round(rep_bytes / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
