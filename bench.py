@@ -328,7 +328,7 @@ def main():
         "repair_GBps": round(rep_bytes / (rep_ms * 1e-3) / 1e9, 2),
         "roofline": {
             "bound": "hbm",
-            "kernel": "encode_kernel_slab (ecwide_amd/csrc/ecw_kernels.hip + ecw_encode_asm.hpp)",
+            "kernel": "encode_kernel_asm (ecwide_amd/csrc/ecw_kernels.hip + ecw_encode_asm.hpp)",
             "achieved": round(achieved, 2),
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",

@@ -11,7 +11,7 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
 SOURCES = [os.path.join(HERE, "csrc", "ecw_codec.cpp"), os.path.join(HERE, "csrc", "ecw_kernels.hip")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("ecw_gf.hpp", "ecw_internal.hpp")] + [
+HEADERS = [os.path.join(HERE, "csrc", f) for f in ("ecw_gf.hpp", "ecw_internal.hpp", "ecw_encode_asm.hpp")] + [
     os.path.join(REPO, "include", "ecwide.h")]
 OUT = os.path.join(HERE, "libecwide.so")
 SHIM_SRC = os.path.join(HERE, "csrc", "ecw_isal_shim.cpp")

@@ -33,7 +33,8 @@
 //   s45 end of the current group, s46 LDS table record of the row, s47/s48
 //   record high/low bytes, s49 scratch, s[50:53] v_perm selectors, s[54:55]
 //   global output row, s56 output index, s57/s58 transpose selectors,
-//   s59 finished groups; v[58:77] parked local parities (tuples start on
+//   s59 finished groups, s60/s61/s62 pointer-table offsets (TAB);
+//   v[58:77] parked local parities (tuples start on
 //   even registers on gfx950).
 #pragma once
 
@@ -114,13 +115,13 @@
 // End of the local group at row s44 (0-based)? Store the local parity,
 // advance to the next local block and group. ZL = 1: reset the XOR.
 #define ECW_BOUNDARY_NONE
-#define ECW_BOUNDARY(ZL)                                  \
+#define ECW_BOUNDARY(ZL, MODE)                            \
   "s_add_u32 s49, s44, 1\n\t"                             \
   "s_cmp_eq_u32 s49, s45\n\t"                             \
   "s_cbranch_scc0 20f\n\t"                                \
+  ECW_LPTR_GET_##MODE                                     \
   ECW_ASM_LSTORE                                          \
-  "s_add_u32 s42, s42, %[bslo]\n\t"                       \
-  "s_addc_u32 s43, s43, %[bshi]\n\t"                      \
+  ECW_LPTR_NEXT_##MODE                                    \
   "s_add_u32 s45, s45, %[r]\n\t"                          \
   "s_min_u32 s45, s45, %[k]\n\t"                          \
   "s_nop 1\n\t"                                           \
@@ -153,17 +154,43 @@
   ECW_LRESET_1                                              \
   "20:\n\t"
 // store parked local t (if t < number of groups) and advance the block
-#define ECW_UNPARK(T, V)                                                    \
+#define ECW_UNPARK(T, V, MODE)                                              \
   "s_cmp_le_u32 s59, " #T "\n\t"                                            \
   "s_cbranch_scc1 27f\n\t"                                                  \
+  ECW_LPTR_GET_##MODE                                                       \
   "global_store_dwordx4 v40, " V ", s[42:43]" ECW_ASM_STMOD "\n\t"          \
-  "s_add_u32 s42, s42, %[bslo]\n\t"                                         \
-  "s_addc_u32 s43, s43, %[bshi]\n\t"
-#define ECW_STORE_PARKED                                                    \
-  "s_mov_b64 s[42:43], %[lrow0]\n\t"                                        \
-  ECW_UNPARK(0, "v[58:61]") ECW_UNPARK(1, "v[62:65]") ECW_UNPARK(2, "v[66:69]") \
-  ECW_UNPARK(3, "v[70:73]") ECW_UNPARK(4, "v[74:77]")                       \
+  ECW_LPTR_NEXT_##MODE
+#define ECW_STORE_PARKED(MODE)                                              \
+  ECW_LPTR_INIT_##MODE                                                      \
+  ECW_UNPARK(0, "v[58:61]", MODE) ECW_UNPARK(1, "v[62:65]", MODE)           \
+  ECW_UNPARK(2, "v[66:69]", MODE) ECW_UNPARK(3, "v[70:73]", MODE)           \
+  ECW_UNPARK(4, "v[74:77]", MODE)                                           \
   "27:\n\t"
+
+// Block pointers. SLAB: %[row0] / %[lrow0] / %[grow0] are the first data,
+// local and global blocks, all %[bslo]/%[bshi] apart. TAB (pointer mode):
+// they are the addresses of pointer tables in the kernel arguments
+// (PtrRows::src, &dst[nrows], &dst[0]), and every block pointer is an
+// s_load. The row pointer for the next ring load is fetched right after the
+// previous load and is ready behind the next row's lgkmcnt(0); the counted
+// lgkmcnt waits inside a row stay correct with an s_load outstanding (LDS
+// returns in order; an extra outstanding op only makes them wait longer).
+#define ECW_ROWPTR_INIT_SLAB "s_mov_b64 s[40:41], %[row0]\n\t"
+#define ECW_ROWPTR_INIT_TAB "s_load_dwordx2 s[40:41], %[row0], 0x0\n\ts_mov_b32 s60, 8\n\ts_waitcnt lgkmcnt(0)\n\t"
+#define ECW_NEXTROW_SLAB "s_add_u32 s40, s40, %[bslo]\n\ts_addc_u32 s41, s41, %[bshi]\n\t"
+#define ECW_NEXTROW_TAB "s_load_dwordx2 s[40:41], %[row0], s60\n\ts_add_u32 s60, s60, 8\n\t"
+#define ECW_LPTR_INIT_SLAB "s_mov_b64 s[42:43], %[lrow0]\n\t"
+#define ECW_LPTR_INIT_TAB "s_mov_b32 s61, 0\n\t"
+#define ECW_LPTR_GET_SLAB
+#define ECW_LPTR_GET_TAB "s_load_dwordx2 s[42:43], %[lrow0], s61\n\ts_waitcnt lgkmcnt(0)\n\t"
+#define ECW_LPTR_NEXT_SLAB "s_add_u32 s42, s42, %[bslo]\n\ts_addc_u32 s43, s43, %[bshi]\n\t"
+#define ECW_LPTR_NEXT_TAB "s_add_u32 s61, s61, 8\n\t"
+#define ECW_GPTR_INIT_SLAB "s_mov_b64 s[54:55], %[grow0]\n\t"
+#define ECW_GPTR_INIT_TAB "s_mov_b32 s62, 0\n\t"
+#define ECW_GPTR_GET_SLAB
+#define ECW_GPTR_GET_TAB "s_load_dwordx2 s[54:55], %[grow0], s62\n\ts_waitcnt lgkmcnt(0)\n\t"
+#define ECW_GPTR_NEXT_SLAB "s_add_u32 s54, s54, %[bslo]\n\ts_addc_u32 s55, s55, %[bshi]\n\t"
+#define ECW_GPTR_NEXT_TAB "s_add_u32 s62, s62, 8\n\t"
 #define ECW_LRESET_0
 #define ECW_LRESET_1 "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t"
 
@@ -180,21 +207,22 @@
 #endif
 #define ECW_LOAD_A "global_load_dwordx4 v[4:7], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_LOAD_B "global_load_dwordx4 v[8:11], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
-#define ECW_NEXTROW "s_add_u32 s40, s40, %[bslo]\n\ts_addc_u32 s41, s41, %[bshi]\n\t"
 #define ECW_ROW_A(XL) ECW_ROW("v4", "v5", "v6", "v7", XL)
 #define ECW_ROW_B(XL) ECW_ROW("v8", "v9", "v10", "v11", XL)
 
-// The whole tile. BND is the boundary code (ECW_BOUNDARY(ZL) or nothing),
-// XL whether rows are XOR-ed into the local parity.
-#define ECW_TILE_ASM(BND, XL, END)                                             \
+// The whole tile. BND is the boundary code (ECW_BOUNDARY(ZL, MODE) or
+// nothing), XL whether rows are XOR-ed into the local parity, END the code
+// after the last row (parked locals), MODE SLAB or TAB.
+#define ECW_TILE_ASM(BND, XL, END, MODE)                                           \
   "v_mov_b32 v40, %[col]\n\t"                                               \
   "v_mov_b32 v33, 0x3c3c3c3c\n\t"                                           \
   "s_mov_b32 s50, 0x0c0c0400\n\t"                                           \
   "s_mov_b32 s51, 0x0c0c0401\n\t"                                           \
   "s_mov_b32 s52, 0x0c0c0402\n\t"                                           \
   "s_mov_b32 s53, 0x0c0c0403\n\t"                                           \
-  "s_mov_b64 s[40:41], %[row0]\n\t"                                         \
-  ECW_LOAD_A ECW_NEXTROW ECW_LOAD_B ECW_NEXTROW                             \
+  ECW_ROWPTR_INIT_##MODE                                                    \
+  ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
+  ECW_LOAD_B ECW_NEXTROW_##MODE                                             \
   "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
   "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
   "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
@@ -203,7 +231,7 @@
   "s_mov_b32 s44, 0\n\t"                                                    \
   "s_mov_b32 s59, 0\n\t"                                                    \
   "s_mov_b32 s46, %[lds]\n\t"                                               \
-  "s_mov_b64 s[42:43], %[lrow0]\n\t"                                        \
+  ECW_LPTR_INIT_##MODE                                                      \
   "s_min_u32 s45, %[r], %[k]\n\t"                                           \
   /* main loop: rows j, j+1 while rows j+2, j+3 exist */                    \
   "10:\n\t"                                                                 \
@@ -211,10 +239,10 @@
   "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
   "s_cbranch_scc1 11f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW                                  \
+  ECW_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW_##MODE                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW                                  \
+  ECW_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW_##MODE                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_branch 10b\n\t"                                                        \
   /* 2 or 3 rows left (k - j); slot A holds row j, slot B row j+1 */        \
@@ -240,7 +268,7 @@
   "13:\n\t"                                                                 \
   END                                                                       \
   /* global rows: byte l of the packed accumulators -> output row l */      \
-  "s_mov_b64 s[54:55], %[grow0]\n\t"                                        \
+  ECW_GPTR_INIT_##MODE                                                      \
   "s_mov_b32 s56, 0\n\t"                                                    \
   "30:\n\t"                                                                 \
   "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
@@ -265,10 +293,10 @@
   "v_perm_b32 v34, v25, v24, s57\n\t"                                       \
   "v_perm_b32 v35, v27, v26, s58\n\t"                                       \
   "v_or_b32 v39, v34, v35\n\t"                                              \
+  ECW_GPTR_GET_##MODE                                                       \
   "global_store_dwordx4 v40, v[36:39], s[54:55]" ECW_ASM_STMOD "\n\t"      \
   "s_nop 1\n\t"                                                             \
-  "s_add_u32 s54, s54, %[bslo]\n\t"                                         \
-  "s_addc_u32 s55, s55, %[bshi]\n\t"                                        \
+  ECW_GPTR_NEXT_##MODE                                                      \
   "s_add_u32 s56, s56, 1\n\t"                                               \
   "s_branch 30b\n\t"                                                        \
   "31:"
@@ -282,7 +310,7 @@
     "v33", "v34", "v35", "v36", "v37", "v38", "v39", "v40", "v41", "v42", "v43", "v44", "v45", "v46",  \
     "v47", "v48", "v49", "v50", "v51", "v52", "v53", "v54", "v55", "v56", "s40", "s41", "s42", "s43", \
     "s44", "s45", "s46", "s47", "s48", "s49", "s50", "s51", "s52", "s53", "s54", "s55", "s56", "s57",  \
-    "s58", "s59", "scc", "memory"
+    "s58", "s59", "s60", "s61", "s62", "scc", "memory"
 
 #define ECW_TILE_OPERANDS_PARK                                                     \
   ECW_TILE_OPERANDS, "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", \
@@ -292,20 +320,29 @@ namespace ecw {
 namespace {
 
 // LOCAL: kLocalNone / kLocalXor / kLocalZero (ecw_internal.hpp); PARK: keep
-// the (<= 5) local parities in registers until the end of the tile. Requires
+// the (<= 5) local parities in registers until the end of the tile; TAB:
+// block pointers come from pointer tables (see ECW_ROWPTR_INIT_TAB). Requires
 // k >= 2, a full tile (every lane's 16 bytes in range) and exec = all lanes.
-template <int LOCAL, bool PARK>
+#define ECW_TILE_CALL(MODE)                                                              \
+  if constexpr (LOCAL == kLocalNone) {                                                   \
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW_TILE_OPERANDS);           \
+  } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_PARK, 1, ECW_STORE_PARKED(MODE), MODE)        \
+                     ECW_TILE_OPERANDS_PARK);                                            \
+  } else if constexpr (LOCAL == kLocalXor) {                                             \
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW_TILE_OPERANDS);       \
+  } else {                                                                               \
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(0, MODE), 0, , MODE) ECW_TILE_OPERANDS);       \
+  }
+
+template <int LOCAL, bool PARK, bool TAB>
 __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
                                                 int k, int r, int nrows, uint32_t lds, uint32_t col) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
-  if constexpr (LOCAL == kLocalNone) {
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_NONE, 0, ) ECW_TILE_OPERANDS);
-  } else if constexpr (LOCAL == kLocalXor && PARK) {
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_PARK, 1, ECW_STORE_PARKED) ECW_TILE_OPERANDS_PARK);
-  } else if constexpr (LOCAL == kLocalXor) {
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(1), 1, ) ECW_TILE_OPERANDS);
+  if constexpr (TAB) {
+    ECW_TILE_CALL(TAB)
   } else {
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(0), 0, ) ECW_TILE_OPERANDS);
+    ECW_TILE_CALL(SLAB)
   }
 }
 

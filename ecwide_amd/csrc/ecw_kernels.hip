@@ -331,7 +331,7 @@ __global__ __launch_bounds__(kBlock, ECW_ENC_MIN_WAVES) void encode_kernel(const
 }
 
 #ifndef ECW_ENC_ASM
-#define ECW_ENC_ASM 1  // slab batches with <= 4 global rows: hand-scheduled tile loop (ecw_encode_asm.hpp)
+#define ECW_ENC_ASM 1  // <= 4 global rows: hand-scheduled tile loop (ecw_encode_asm.hpp)
 #endif
 #ifndef ECW_ASM_MIN_WAVES
 #define ECW_ASM_MIN_WAVES 6  // 80 VGPRs: the parked asm tile uses 77 (6 measured >= 8 also without parking)
@@ -344,13 +344,17 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
   return reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
 }
 
-// Slab encode with <= 4 global rows (one u32 table entry per nibble) and
-// k >= 2: full tiles through the hand-scheduled asm tile, the ragged last
-// tile of a block through encode_tile<..., TAIL>. PARK (<= 5 groups): local
-// parities are stored at the end of each tile (ecw_encode_asm.hpp).
-template <int LOCAL, bool PARK>
-__global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_slab(const SlabRows rows, const EncodeGeom g,
-                                                                               const uint4* __restrict__ tbl) {
+// Encode with <= 4 global rows (one u32 table entry per nibble) and k >= 2:
+// full tiles through the hand-scheduled asm tile, the ragged last tile of a
+// block through encode_tile<..., TAIL>. PARK (<= 5 groups): local parities
+// are stored at the end of each tile (ecw_encode_asm.hpp). Pointer mode
+// hands the asm the addresses of the pointer tables in the kernel
+// arguments: `rows` is the first argument, so it sits at offset 0 of the
+// kernarg segment (taking the address of the by-value argument itself
+// would make the compiler copy all 3 KiB of it to scratch).
+template <int LOCAL, bool PARK, class Rows>
+__global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_asm(const Rows rows, const EncodeGeom g,
+                                                                              const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int n16 = g.k * 8;
   for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
@@ -359,16 +363,26 @@ __global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_slab(
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
-  const uint64_t bs = rows.bstride;
   for (uint64_t tile = g.tile_begin + blockIdx.x; tile < g.tile_end; tile += gridDim.x) {
     const TileAt cur = tile_at(g, tile);
     if (cur.full) {
-      const uint64_t so = static_cast<uint64_t>(cur.s) * rows.sstride;
-      const uint8_t* sb = uniform_ptr(rows.base + so);
-      const uint8_t* pb = uniform_ptr(rows.pbase + so);
-      encode_tile_asm<LOCAL, PARK>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
-                                   const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * bs), bs, k, r, nrows,
-                                   __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+      if constexpr (std::is_same<Rows, SlabRows>::value) {
+        const uint64_t bs = rows.bstride;
+        const uint64_t so = static_cast<uint64_t>(cur.s) * rows.sstride;
+        const uint8_t* sb = uniform_ptr(rows.base + so);
+        const uint8_t* pb = uniform_ptr(rows.pbase + so);
+        encode_tile_asm<LOCAL, PARK, false>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
+                                            const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * bs), bs, k, r,
+                                            nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+      } else {
+        const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
+            reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
+        const uint8_t* dtab = ka + offsetof(PtrRows, dst);
+        encode_tile_asm<LOCAL, PARK, true>(ka + offsetof(PtrRows, src),
+                                           const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
+                                           const_cast<uint8_t*>(dtab), 0, k, r, nrows,
+                                           __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+      }
     } else {
       uint4 ring[kPrefetchEncAsmTail];
       ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
@@ -495,20 +509,21 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
   return hipGetLastError();
 }
 
-hipError_t launch_encode_slab_asm(const SlabRows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
+template <class Rows>
+hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
   const size_t lds = static_cast<size_t>(g.k) * 128;
   switch (g.local_mode) {
     case kLocalXor:
       if (g.groups <= kMaxParkedLocals)
-        hipLaunchKernelGGL((encode_kernel_slab<kLocalXor, true>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, true, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       else
-        hipLaunchKernelGGL((encode_kernel_slab<kLocalXor, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      hipLaunchKernelGGL((encode_kernel_slab<kLocalZero, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      hipLaunchKernelGGL((encode_kernel_asm<kLocalZero, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       break;
     default:
-      hipLaunchKernelGGL((encode_kernel_slab<kLocalNone, false>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      hipLaunchKernelGGL((encode_kernel_asm<kLocalNone, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
   }
   return hipGetLastError();
 }
@@ -530,12 +545,10 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
     g.tile_end = t0 + win < total ? t0 + win : total;
     const dim3 grid(grid_for(g.tile_end - g.tile_begin));
     hipError_t e;
-    if constexpr (std::is_same<Rows, SlabRows>::value) {
-      if (ECW_ENC_ASM && g.nrows <= 4 && g.k >= 2) {
-        e = launch_encode_slab_asm(rows, g, tbl, grid, s);
-        if (e != hipSuccess) return e;
-        continue;
-      }
+    if (ECW_ENC_ASM && g.nrows <= 4 && g.k >= 2) {
+      e = launch_encode_asm(rows, g, tbl, grid, s);
+      if (e != hipSuccess) return e;
+      continue;
     }
     e = g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
     if (e != hipSuccess) return e;

@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--code", default="C", help="C (CL, locals) or R (RS, globals only)")
     ap.add_argument("--pad", type=int, default=4096, help="block stride = B + pad (rounded to 256)")
+    ap.add_argument("--ptr", action="store_true",
+                    help="encode each stripe with ecw_encode_dev and its blocks in reverse order "
+                         "(pointer mode, not one stride apart)")
     ap.add_argument("--chunk", type=int, default=0,
                     help="chunk-interleaved layout: each stripe stored as B/CHUNK column chunks, "
                          "the k+m+g blocks' chunks adjacent (timed as B/CHUNK mini-stripes)")
@@ -66,6 +69,11 @@ def main():
         assert libs[0][1].ecw_encode_batch_dev(libs[0][2], c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream) == 0
         torch.cuda.synchronize()
         ref = buf[(k) * bstride:(k) * bstride + B].clone()
+    if a.ptr:
+        base = buf.data_ptr()
+        dptrs = [(c_void_p * k)(*[base + s_ * sstride + (k - 1 - j) * bstride for j in range(k)]) for s_ in range(S)]
+        pptrs = [(c_void_p * (m + g))(*[base + s_ * sstride + (nblk - 1 - i) * bstride for i in range(m + g)])
+                 for s_ in range(S)]
     res = {n: ([], []) for n, _, _ in libs}
     for rd in range(a.rounds):
         for name, L, h in libs:
@@ -73,8 +81,13 @@ def main():
             for it in range(a.iters + 1):
                 if it == 1:
                     e[0].record()
-                st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
-                assert st == 0, (name, st)
+                if a.ptr:
+                    for s_ in range(S):
+                        st = L.ecw_encode_dev(h, dptrs[s_], pptrs[s_], B, stream)
+                        assert st == 0, (name, st)
+                else:
+                    st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
+                    assert st == 0, (name, st)
             e[1].record()
             for it in range(a.iters if a.code == "C" else 0):
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
