@@ -167,6 +167,30 @@
   ECW_UNPARK(4, "v[74:77]", MODE)                                           \
   "27:\n\t"
 
+// ECWide-C literal mode (every L block is zeros): the rows only count the
+// finished groups, and the end of the tile stores v[28:31] (zero throughout)
+// once per group -- the same end-of-tile placement as the parked parities,
+// for any number of groups.
+#define ECW_BOUNDARY_COUNT                                  \
+  "s_add_u32 s49, s44, 1\n\t"                               \
+  "s_cmp_eq_u32 s49, s45\n\t"                               \
+  "s_cbranch_scc0 20f\n\t"                                  \
+  "s_add_u32 s59, s59, 1\n\t"                               \
+  "s_add_u32 s45, s45, %[r]\n\t"                            \
+  "s_min_u32 s45, s45, %[k]\n\t"                            \
+  "20:\n\t"
+#define ECW_STORE_ZEROS(MODE)                                               \
+  ECW_LPTR_INIT_##MODE                                                      \
+  "28:\n\t"                                                                 \
+  "s_cmp_eq_u32 s59, 0\n\t"                                                 \
+  "s_cbranch_scc1 29f\n\t"                                                  \
+  ECW_LPTR_GET_##MODE                                                       \
+  "global_store_dwordx4 v40, v[28:31], s[42:43]" ECW_ASM_STMOD "\n\t"       \
+  ECW_LPTR_NEXT_##MODE                                                      \
+  "s_sub_u32 s59, s59, 1\n\t"                                               \
+  "s_branch 28b\n\t"                                                        \
+  "29:\n\t"
+
 // Block pointers. SLAB: %[row0] / %[lrow0] / %[grow0] are the first data,
 // local and global blocks, all %[bslo]/%[bshi] apart. TAB (pointer mode):
 // they are the addresses of pointer tables in the kernel arguments
@@ -320,7 +344,8 @@ namespace ecw {
 namespace {
 
 // LOCAL: kLocalNone / kLocalXor / kLocalZero (ecw_internal.hpp); PARK: keep
-// the (<= 5) local parities in registers until the end of the tile; TAB:
+// the (<= 5) local parities in registers until the end of the tile (literal
+// mode always stores its zero L blocks there); TAB:
 // block pointers come from pointer tables (see ECW_ROWPTR_INIT_TAB). Requires
 // k >= 2, a full tile (every lane's 16 bytes in range) and exec = all lanes.
 #define ECW_TILE_CALL(MODE)                                                              \
@@ -332,7 +357,8 @@ namespace {
   } else if constexpr (LOCAL == kLocalXor) {                                             \
     asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW_TILE_OPERANDS);       \
   } else {                                                                               \
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(0, MODE), 0, , MODE) ECW_TILE_OPERANDS);       \
+    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)          \
+                     ECW_TILE_OPERANDS);                                                 \
   }
 
 template <int LOCAL, bool PARK, bool TAB>

@@ -224,6 +224,44 @@ def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S):
             assert torch.equal(out[st * o:st * o + B], slab.block(st, lost)), (lost, st)
 
 
+def test_random_sweep_vs_oracle(E, torch, orc):
+    """Seeded random CL shapes (k, m, r, B, stripes, local mode) against the
+    oracle: covers the asm tile's row loop / 2-3-row epilogue / group
+    boundaries / parked and unparked locals / ragged tails in combination,
+    in slab mode and in pointer mode (block j stored at slot k-1-j, so the
+    pointers are not one stride apart)."""
+    rng = np.random.default_rng(2026)
+    for trial in range(24):
+        k = int(rng.integers(2, 160))
+        m = int(rng.integers(1, 5))
+        r = int(rng.integers(1, k + 1))
+        B = int(rng.choice([4096, 8192, 4096 * int(rng.integers(1, 4)) + 16 * int(rng.integers(1, 256))]))
+        S = int(rng.integers(1, 3))
+        literal = trial % 4 == 3
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False,
+                                     local_mode="literal" if literal else "xor")
+        oc = orc.codec("C", k, m, r, B)
+        slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+        slab.fill_random(seed=1000 + trial)
+        slab.encode()
+        torch.cuda.synchronize()
+        wants = []
+        for st in range(S):
+            want = oc.encode([orc.fill(B, 1000 + trial, st, j) for j in range(k)], literal=literal, threads=8)
+            wants.append(want)
+            for i, p in enumerate(slab.parity(st)):
+                assert np.array_equal(p.cpu().numpy(), want[i]), (trial, k, m, r, B, st, i)
+        np_ = c.parityNum
+        dbuf = torch.empty((k, B), dtype=torch.uint8, device="cuda")
+        pbuf = torch.full((np_, B), 0x5A, dtype=torch.uint8, device="cuda")
+        for j in range(k):
+            dbuf[k - 1 - j].copy_(slab.block(0, j))
+        c.encodeData([dbuf[k - 1 - j] for j in range(k)], [pbuf[np_ - 1 - i] for i in range(np_)])
+        torch.cuda.synchronize()
+        for i in range(np_):
+            assert np.array_equal(pbuf[np_ - 1 - i].cpu().numpy(), wants[0][i]), ("ptr", trial, k, m, r, B, i)
+
+
 @pytest.mark.parametrize("B", [(20 << 20) + 37, (8 << 20), 4096 * 3 + 5])
 def test_host_pipeline_multi_chunk_and_repair(E, torch, orc, B):
     """ecw_encode / ecw_repair on host buffers larger than one 8 MiB pipeline
