@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--check", action="store_true")
     ap.add_argument("--code", default="C", help="C (CL, locals) or R (RS, globals only)")
     ap.add_argument("--pad", type=int, default=4096, help="block stride = B + pad (rounded to 256)")
+    ap.add_argument("--literal", action="store_true", help="ECWide-C literal local mode (zero L blocks)")
     ap.add_argument("--ptr", action="store_true",
                     help="encode each stripe with ecw_encode_dev and its blocks in reverse order "
                          "(pointer mode, not one stride apart)")
@@ -58,7 +59,7 @@ def main():
         sch = _lib.ecw_scheme()
         assert L.ecw_scheme_init(byref(sch), a.code.encode(), k, m, r, B) == 0
         h = c_void_p()
-        assert L.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(h)) == 0
+        assert L.ecw_codec_create(byref(sch), 1, 0, 1 if a.literal else 0, 0, byref(h)) == 0
         libs.append((os.path.basename(path), L, h))
     L0 = libs[0][1]
     assert L0.ecw_fill_random_dev(0, c_void_p(buf.data_ptr()), bstride, sstride, S, k, B, 1, 0, 0, stream) == 0
@@ -89,7 +90,7 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            for it in range(a.iters if a.code == "C" else 0):
+            for it in range(a.iters if a.code == "C" and not a.literal else 0):  # literal L blocks cannot repair
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
                                             c_void_p(out.data_ptr()), B, B, stream)
                 assert st == 0, (name, st)
