@@ -12,11 +12,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <functional>
 #include <map>
 #include <mutex>
 #include <new>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/ecwide.h"
@@ -68,12 +70,15 @@ struct ecw_codec {
   struct HostPipe* pipe = nullptr;    // streams/events of the host-memory pipeline
   uint8_t* d_stage = nullptr;
   size_t stage_bytes = 0;
+  uint8_t* h_stage = nullptr;         // pinned host staging of the small-block path
+  size_t h_stage_bytes = 0;
 
   ~ecw_codec() {
     if (dev_ready) {
       DeviceGuard g(device);
       for (void* p : d_pass) (void)hipFree(p);
       if (d_stage) (void)hipFree(d_stage);
+      if (h_stage) (void)hipHostFree(h_stage);
       if (stream) (void)hipStreamDestroy(stream);
       destroy_pipe();
     }
@@ -113,6 +118,16 @@ struct ecw_codec {
     stage_bytes = 0;
     if (hipMalloc(&d_stage, bytes) != hipSuccess) return ECW_ENOMEM;
     stage_bytes = bytes;
+    return ECW_OK;
+  }
+  int ensure_host_stage(size_t bytes) {
+    if (h_stage_bytes >= bytes) return ECW_OK;
+    if (h_stage) (void)hipHostFree(h_stage);
+    h_stage = nullptr;
+    h_stage_bytes = 0;
+    if (hipHostMalloc(reinterpret_cast<void**>(&h_stage), bytes, hipHostMallocDefault) != hipSuccess)
+      return ECW_ENOMEM;
+    h_stage_bytes = bytes;
     return ECW_OK;
   }
 };
@@ -766,6 +781,80 @@ int ecw_partial_decode(ecw_codec* c, const uint8_t* const* data, uint8_t* target
 // through the same 3-slot / 3-stream pipeline as host_roundtrip, each slot
 // laid out as a slab ([D.., G.., L..] per stripe) so one launch encodes the
 // whole batch.
+namespace {
+
+// Small blocks (ECWide-H's 4 KiB chunks): one copy call per block would cost
+// more than the block (~5 us of API time each), so a batch of stripes is
+// packed by the CPU into pinned host memory laid out like the device slab,
+// crosses PCIe as one 2-D copy each way, and is encoded in one launch. Two
+// staging slots: the CPU packs batch b+1 (and unpacks batch b-1) while the
+// GPU copies and encodes batch b.
+constexpr size_t kSmallBlock = size_t(256) << 10;
+constexpr size_t kPackBytes = size_t(32) << 20;  // host + device slot size
+
+void copy_blocks(size_t n, const std::function<void(size_t, size_t)>& fn) {
+  // parallel memcpy loop for big batches (a thread costs ~20 us to start)
+  const size_t nt = std::min<size_t>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
+  if (n < 64 || nt < 2) return fn(0, n);
+  std::vector<std::thread> th;
+  const size_t per = (n + nt - 1) / nt;
+  for (size_t t = 1; t < nt && t * per < n; ++t) th.emplace_back(fn, t * per, std::min(n, (t + 1) * per));
+  fn(0, std::min(n, per));
+  for (auto& x : th) x.join();
+}
+
+int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t* const* data,
+                          uint8_t* const* parity, size_t len) {
+  const int k = c->k(), np = c->info.parity_num, nb = k + np;
+  const size_t cs = (len + 255) & ~static_cast<size_t>(255);  // block stride in the slot
+  const size_t sb_bytes = cs * nb;
+  const int per = static_cast<int>(std::max<size_t>(1, std::min<size_t>(stripes, kPackBytes / sb_bytes)));
+  const size_t slot = sb_bytes * per;
+  int st;
+  if ((st = c->ensure_stage(slot * 2)) || (st = c->ensure_host_stage(slot * 2))) return st;
+  int first[2] = {-1, -1}, count[2] = {0, 0};  // batch held by each slot, awaiting unpack
+  auto unpack = [&](int q) -> int {
+    if (first[q] < 0) return ECW_OK;
+    if (hipEventSynchronize(P.ev_out[q]) != hipSuccess) return ECW_EDEVICE;
+    const uint8_t* h = c->h_stage + q * slot;
+    const int s0 = first[q];
+    copy_blocks(static_cast<size_t>(count[q]) * np, [&](size_t a, size_t b) {
+      for (size_t x = a; x < b; ++x)
+        std::memcpy(parity[static_cast<size_t>(s0) * np + x], h + (x / np) * sb_bytes + (k + x % np) * cs, len);
+    });
+    first[q] = -1;
+    return ECW_OK;
+  };
+  int b = 0;
+  for (int s0 = 0; s0 < stripes; s0 += per, ++b) {
+    const int q = b & 1, ns = std::min(per, stripes - s0);
+    if ((st = unpack(q))) return st;
+    uint8_t* h = c->h_stage + q * slot;
+    uint8_t* d = c->d_stage + q * slot;
+    copy_blocks(static_cast<size_t>(ns) * k, [&](size_t a, size_t e) {
+      for (size_t x = a; x < e; ++x)
+        std::memcpy(h + (x / k) * sb_bytes + (x % k) * cs, data[static_cast<size_t>(s0) * k + x], len);
+    });
+    if (hipMemcpy2DAsync(d, sb_bytes, h, sb_bytes, k * cs, ns, hipMemcpyHostToDevice, P.s_run) != hipSuccess)
+      return ECW_EDEVICE;
+    const SlabRows slab = slab_rows(d, cs, sb_bytes, k);
+    EncodeTarget t;
+    t.slab = &slab;
+    t.stripes = ns;
+    if ((st = run_encode(c, t, len, P.s_run))) return st;
+    if (hipMemcpy2DAsync(h + k * cs, sb_bytes, d + k * cs, sb_bytes, np * cs, ns, hipMemcpyDeviceToHost,
+                         P.s_run) != hipSuccess ||
+        hipEventRecord(P.ev_out[q], P.s_run) != hipSuccess)
+      return ECW_EDEVICE;
+    first[q] = s0;
+    count[q] = ns;
+  }
+  if ((st = unpack(b & 1)) || (st = unpack((b + 1) & 1))) return st;
+  return ECW_OK;
+}
+
+}  // namespace
+
 int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, uint8_t* const* parity,
                        size_t len) {
   if (!c || stripes < 0 || !data || !parity || !check_len(len)) return ECW_EINVAL;
@@ -786,6 +875,7 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
   }
   HostPipe& P = *c->pipe;
   if ((st = P.init())) return st;
+  if (len <= kSmallBlock) return encode_stripes_packed(c, P, stripes, data, parity, len);
   const size_t chunk = std::min(len, kHostChunk);
   const size_t cstride = (chunk + 255) & ~static_cast<size_t>(255);
   const size_t stripe_bytes = cstride * nb;

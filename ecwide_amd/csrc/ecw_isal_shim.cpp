@@ -12,8 +12,18 @@
 // isal:erasure_code/ec_base.c:290-305) and runs a cached matrix codec
 // (ecw_matrix_codec_create) through the host-memory pipeline.
 //
+// Concurrent callers are batched (group commit): ECWide-H calls
+// ec_encode_data on 4 KiB chunks from four proxy threads
+// (ECWide-H/proxy/proxy.cpp:2001-2012), and one GPU round trip costs far more
+// than 4 KiB of work. A call joins the pending list of its (codec, len); if
+// no batch of that key is running, the caller runs everything pending as one
+// ecw_encode_stripes call (one launch, packed copies); otherwise it waits and
+// is picked up by the next batch. A lone caller runs at once -- there is no
+// timer. ECW_ISAL_BATCH=0 turns batching off (one ecw_encode per call).
+//
 // The ISA-L functions return void; a failure is reported on stderr and by
 // ecw_isal_last_status() (per thread), never by exit().
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -28,10 +38,26 @@
 
 namespace {
 
+// Pending calls of one (codec, len); see the group commit above.
+struct Batcher {
+  struct Req {
+    unsigned char** data;
+    unsigned char** coding;
+    int status = ECW_OK;
+    bool done = false;
+  };
+  std::mutex mu;
+  std::condition_variable cv;
+  std::vector<Req*> pending;
+  bool running = false;
+};
+
 struct Cache {
   std::mutex mu;
   std::map<std::string, ecw_codec*> codecs;  // key: k, rows, matrix bytes
+  std::map<std::pair<ecw_codec*, int>, Batcher*> batchers;
   ~Cache() {
+    for (auto& kv : batchers) delete kv.second;
     for (auto& kv : codecs) ecw_codec_destroy(kv.second);
   }
 };
@@ -63,6 +89,57 @@ ecw_codec* codec_for(int k, int rows, const unsigned char* gftbls) {
   if (t_status != ECW_OK) return nullptr;
   c.codecs.emplace(key, cd);
   return cd;
+}
+
+bool batching_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("ECW_ISAL_BATCH");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+Batcher& batcher_for(ecw_codec* cd, int len) {
+  Cache& c = cache();
+  std::lock_guard<std::mutex> lk(c.mu);
+  Batcher*& b = c.batchers[{cd, len}];
+  if (!b) b = new Batcher();
+  return *b;
+}
+
+int encode_batched(ecw_codec* cd, int len, int k, int rows, unsigned char** data, unsigned char** coding) {
+  Batcher& b = batcher_for(cd, len);
+  Batcher::Req r{data, coding};
+  std::unique_lock<std::mutex> lk(b.mu);
+  b.pending.push_back(&r);
+  while (!r.done) {
+    if (b.running) {
+      b.cv.wait(lk);
+      continue;
+    }
+    b.running = true;
+    std::vector<Batcher::Req*> batch;
+    batch.swap(b.pending);
+    lk.unlock();
+    std::vector<const uint8_t*> dp;
+    std::vector<uint8_t*> pp;
+    dp.reserve(batch.size() * k);
+    pp.reserve(batch.size() * rows);
+    for (const Batcher::Req* q : batch) {
+      dp.insert(dp.end(), q->data, q->data + k);
+      pp.insert(pp.end(), q->coding, q->coding + rows);
+    }
+    const int st = ecw_encode_stripes(cd, static_cast<int>(batch.size()), dp.data(), pp.data(),
+                                      static_cast<size_t>(len));
+    lk.lock();
+    for (Batcher::Req* q : batch) {
+      q->status = st;
+      q->done = true;
+    }
+    b.running = false;
+    b.cv.notify_all();
+  }
+  return r.status;
 }
 
 void report(const char* fn, int st) {
@@ -152,6 +229,7 @@ void ec_encode_data(int len, int k, int rows, unsigned char* g_tbls, unsigned ch
   if (len <= 0 || rows <= 0) return;
   ecw_codec* cd = codec_for(k, rows, g_tbls);
   if (!cd) return report("ec_encode_data", t_status);
+  if (batching_on()) return report("ec_encode_data", encode_batched(cd, len, k, rows, data, coding));
   report("ec_encode_data", ecw_encode(cd, data, coding, static_cast<size_t>(len)));
 }
 

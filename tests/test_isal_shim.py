@@ -160,3 +160,39 @@ def test_encode_stripes_batch(orc):
     for s in (0, 1, 137, S - 1):
         want = oc.encode(data[s])
         assert all(np.array_equal(a, b) for a, b in zip(par[s], want)), s
+
+
+@pytest.mark.gpu
+def test_ec_encode_data_concurrent_callers(shim, orc):
+    """ECWide-H calls ec_encode_data from several proxy threads at once
+    (proxy.cpp:2001-2012): concurrent calls are batched into one GPU launch
+    (group commit) and every caller still gets exactly its own parities."""
+    import threading
+
+    k, m = 11, 3
+    full = np.zeros((k + m) * k, np.uint8)
+    shim.gf_gen_cauchy1_matrix(p(full), k + m, k)
+    tbl = np.zeros(32 * k * m, np.uint8)
+    shim.ec_init_tables(k, m, p(full[k * k:].copy()), p(tbl))
+    rng = np.random.default_rng(7)
+    lens = [4096, 4096, 4096, 1000, 4096, 65536, 4096, 4096]
+    jobs = [[[rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k)] for _ in range(25)] for ln in lens]
+    outs = [[[np.zeros(ln, np.uint8) for _ in range(m)] for _ in range(25)] for ln in lens]
+    errors = []
+
+    def worker(t):
+        for d, o in zip(jobs[t], outs[t]):
+            shim.ec_encode_data(lens[t], k, m, p(tbl), pp(d), pp(o))
+            if shim.ecw_isal_last_status() != 0:
+                errors.append((t, shim.ecw_isal_last_status()))
+
+    th = [threading.Thread(target=worker, args=(t,)) for t in range(len(lens))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=120)
+    assert not errors
+    for t in range(len(lens)):
+        for d, o in zip(jobs[t], outs[t]):
+            want = orc.encode_data(tbl, d, m)
+            assert all(np.array_equal(a, b) for a, b in zip(o, want)), t
