@@ -662,6 +662,7 @@ int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t 
 // copies are DMA at PCIe rate; pageable buffers work too (HIP stages them).
 // Serialised per codec (the staging slots are per codec).
 constexpr size_t kHostChunk = size_t(8) << 20;
+constexpr size_t kSmallBlock = size_t(256) << 10;  // blocks up to this size take the packed path
 constexpr int kSlots = 3;
 
 struct HostPipe {
@@ -761,6 +762,8 @@ static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout
 
 int ecw_encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
   if (!c || !data || !parity || !check_len(len)) return ECW_EINVAL;
+  // small blocks: one packed stripe (two copy calls instead of one per block)
+  if (len > 0 && len <= kSmallBlock) return ecw_encode_stripes(c, 1, data, parity, len);
   return host_roundtrip(c, data, c->k(), parity, c->info.parity_num, len, op_encode);
 }
 
@@ -789,13 +792,13 @@ namespace {
 // crosses PCIe as one 2-D copy each way, and is encoded in one launch. Two
 // staging slots: the CPU packs batch b+1 (and unpacks batch b-1) while the
 // GPU copies and encodes batch b.
-constexpr size_t kSmallBlock = size_t(256) << 10;
 constexpr size_t kPackBytes = size_t(32) << 20;  // host + device slot size
 
-void copy_blocks(size_t n, const std::function<void(size_t, size_t)>& fn) {
-  // parallel memcpy loop for big batches (a thread costs ~20 us to start)
+void copy_blocks(size_t n, size_t len, const std::function<void(size_t, size_t)>& fn) {
+  // parallel memcpy loop for big batches only: a thread costs tens of us to
+  // start, one core copies ~8 MiB in about a millisecond
   const size_t nt = std::min<size_t>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
-  if (n < 64 || nt < 2) return fn(0, n);
+  if (n * len < (size_t(8) << 20) || nt < 2) return fn(0, n);
   std::vector<std::thread> th;
   const size_t per = (n + nt - 1) / nt;
   for (size_t t = 1; t < nt && t * per < n; ++t) th.emplace_back(fn, t * per, std::min(n, (t + 1) * per));
@@ -818,7 +821,7 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
     if (hipEventSynchronize(P.ev_out[q]) != hipSuccess) return ECW_EDEVICE;
     const uint8_t* h = c->h_stage + q * slot;
     const int s0 = first[q];
-    copy_blocks(static_cast<size_t>(count[q]) * np, [&](size_t a, size_t b) {
+    copy_blocks(static_cast<size_t>(count[q]) * np, len, [&](size_t a, size_t b) {
       for (size_t x = a; x < b; ++x)
         std::memcpy(parity[static_cast<size_t>(s0) * np + x], h + (x / np) * sb_bytes + (k + x % np) * cs, len);
     });
@@ -831,7 +834,7 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
     if ((st = unpack(q))) return st;
     uint8_t* h = c->h_stage + q * slot;
     uint8_t* d = c->d_stage + q * slot;
-    copy_blocks(static_cast<size_t>(ns) * k, [&](size_t a, size_t e) {
+    copy_blocks(static_cast<size_t>(ns) * k, len, [&](size_t a, size_t e) {
       for (size_t x = a; x < e; ++x)
         std::memcpy(h + (x / k) * sb_bytes + (x % k) * cs, data[static_cast<size_t>(s0) * k + x], len);
     });
