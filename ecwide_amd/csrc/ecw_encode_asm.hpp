@@ -1,5 +1,5 @@
 // Hand-scheduled encode of ONE full column tile (gfx950 / CDNA4), used by
-// encode_kernel_slab for slab batches with <= 4 global rows per pass.
+// encode_kernel_asm for every encode pass with <= 4 global rows (slab or pointer mode).
 //
 // Same arithmetic as encode_tile() in ecw_kernels.hip (ISA-L's 4-bit split
 // GF(2^8) products, gf_vect_mul_init, isal:erasure_code/ec_base.c:157-262,
