@@ -158,7 +158,7 @@
   "s_cmp_le_u32 s59, " #T "\n\t"                                            \
   "s_cbranch_scc1 27f\n\t"                                                  \
   ECW_LPTR_GET_##MODE                                                       \
-  "global_store_dwordx4 v40, " V ", s[42:43]" ECW_ASM_STMOD "\n\t"          \
+  ECW_ASM_GSTORE(V, "s[42:43]")                                             \
   ECW_LPTR_NEXT_##MODE
 #define ECW_STORE_PARKED(MODE)                                              \
   ECW_LPTR_INIT_##MODE                                                      \
@@ -185,7 +185,7 @@
   "s_cmp_eq_u32 s59, 0\n\t"                                                 \
   "s_cbranch_scc1 29f\n\t"                                                  \
   ECW_LPTR_GET_##MODE                                                       \
-  "global_store_dwordx4 v40, v[28:31], s[42:43]" ECW_ASM_STMOD "\n\t"       \
+  ECW_ASM_GSTORE("v[28:31]", "s[42:43]")                                    \
   ECW_LPTR_NEXT_##MODE                                                      \
   "s_sub_u32 s59, s59, 1\n\t"                                               \
   "s_branch 28b\n\t"                                                        \
@@ -218,8 +218,13 @@
 #define ECW_LRESET_0
 #define ECW_LRESET_1 "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t"
 
+#ifndef ECW_ASM_DIAG_NOSTORE
+#define ECW_ASM_GSTORE(V, S) "global_store_dwordx4 v40, " V ", " S ECW_ASM_STMOD "\n\t"
+#else
+#define ECW_ASM_GSTORE(V, S)  // diagnostic builds only: the encode's reads and math without any store
+#endif
 #ifndef ECW_ASM_DIAG_NOLSTORE
-#define ECW_ASM_LSTORE "global_store_dwordx4 v40, v[28:31], s[42:43]" ECW_ASM_STMOD "\n\t"
+#define ECW_ASM_LSTORE ECW_ASM_GSTORE("v[28:31]", "s[42:43]")
 #else
 #define ECW_ASM_LSTORE  // diagnostic builds only: time the encode without its local-parity stores
 #endif
@@ -318,7 +323,7 @@
   "v_perm_b32 v35, v27, v26, s58\n\t"                                       \
   "v_or_b32 v39, v34, v35\n\t"                                              \
   ECW_GPTR_GET_##MODE                                                       \
-  "global_store_dwordx4 v40, v[36:39], s[54:55]" ECW_ASM_STMOD "\n\t"      \
+  ECW_ASM_GSTORE("v[36:39]", "s[54:55]")                                    \
   "s_nop 1\n\t"                                                             \
   ECW_GPTR_NEXT_##MODE                                                      \
   "s_add_u32 s56, s56, 1\n\t"                                               \
