@@ -115,7 +115,14 @@ __global__ __launch_bounds__(256) void rows_st_kernel(uint8_t* base, uint64_t bs
           __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(const_cast<uint8_t*>(p) + (uint64_t)(k + i) * bstride));
         else if (SM == 1)
           *reinterpret_cast<u32x4*>(const_cast<uint8_t*>(p) + (uint64_t)(k + i) * bstride) = acc[i];
-        else
+        else if (SM >= 3) {
+          u32x4* q = reinterpret_cast<u32x4*>(const_cast<uint8_t*>(p) + (uint64_t)(k + i) * bstride);
+          if (SM == 3) asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(q), "v"(acc[i]) : "memory");
+          if (SM == 4) asm volatile("global_store_dwordx4 %0, %1, off nt sc1" ::"v"(q), "v"(acc[i]) : "memory");
+          if (SM == 5) asm volatile("global_store_dwordx4 %0, %1, off nt sc0 sc1" ::"v"(q), "v"(acc[i]) : "memory");
+          if (SM == 6) asm volatile("global_store_dwordx4 %0, %1, off nt sc0" ::"v"(q), "v"(acc[i]) : "memory");
+          if (SM == 7) asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(q), "v"(acc[i]) : "memory");
+        } else
           __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(out + tile * 32768 + (threadIdx.x / 64) * 8192 +
                                                                          i * 1024 + (threadIdx.x % 64) * 16));
       }
@@ -208,7 +215,7 @@ int main(int argc, char** argv) {
     std::printf("rows_st sm=%d grid=%u  %8.1f GB/s (136 rows counted)\n", SM, grid, sbytes / ms / 1e6);     \
   }
   for (int rep = 0; rep < 2; ++rep) {
-    RSM(0, 65536) RSM(1, 65536) RSM(2, 65536) RSM(0, 0) RSM(1, 0) RSM(2, 0)
+    RSM(0, 65536) RSM(1, 65536) RSM(3, 65536) RSM(4, 65536) RSM(5, 65536) RSM(6, 65536) RSM(7, 65536)
   }
   if (argc > 4) return 0;
   for (int rep = 0; rep < 2; ++rep) {
