@@ -221,11 +221,20 @@ def main():
         args.block_mib = float(int(0.97 * free) // per_mib)
         assert args.block_mib >= 1, f"{free} B free: too small for {S} stripes"
     B = int(args.block_mib * (1 << 20))
-    from ecwide_amd.shard import stripe_shard, weak_shard
+    from ecwide_amd.shard import column_shard, stripe_shard, weak_shard
 
     S_total = S if args.strong else S * world
-    # each rank owns distinct stripe ids; no data exchange between ranks
-    s0, S = stripe_shard(S_total, world, rank) if args.strong else weak_shard(S, rank)
+    B_full = B
+    columns = args.strong and S_total < world
+    if columns:
+        # fewer stripes than GPUs (SURVEY §8e fallback): every rank takes its
+        # byte columns of every stripe instead
+        s0 = 0
+        B = column_shard(B_full, world, rank)[1]
+        assert B > 0, "more GPUs than 4 KiB column tiles"
+    else:
+        # each rank owns distinct stripe ids; no data exchange between ranks
+        s0, S = stripe_shard(S_total, world, rank) if args.strong else weak_shard(S, rank)
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
     codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local)
@@ -271,7 +280,7 @@ def main():
     rep_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
 
     ok = None
-    if args.verify and rank == 0:
+    if args.verify and rank == 0 and not columns:
         import numpy as np
 
         import oracle
@@ -290,7 +299,9 @@ def main():
             dist.destroy_process_group()
         return
 
-    total_bytes = step_bytes // S * S_total * args.steps  # every stripe costs the same bytes
+    # every stripe costs the same bytes; in column mode each stripe's bytes are
+    # spread over the ranks in proportion to their column slices
+    total_bytes = step_bytes * B_full // B // S * S_total * args.steps
     value = total_bytes / el_max / 1e9
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
     traffic = None
@@ -317,9 +328,10 @@ def main():
         "data": "synthetic (counter PRNG, uniform random bytes, generated in HBM)",
         "config": {
             "workload": (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S} stripes/GPU: batched encode + "
-                         f"repair of D0") + (f" [strong: {S_total} stripes in total]" if args.strong else "") + (" [configs[3]: 256 stripes filling HBM, "
+                         f"repair of D0") + (f" [strong: {S_total} stripes in total]" if args.strong else "")
+            + (f" [column-sliced: {B} of {B_full} B per block on this rank]" if columns else "") + (" [configs[3]: 256 stripes filling HBM, "
                                              f"{slab.buf.numel() / 2**30:.1f} GiB slab]" if args.hbm_fill else ""),
-            "k": k, "r": r, "m": m, "g": g, "block_bytes": B, "stripes_per_gpu": S, "stripes_total": S_total,
+            "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B, "stripes_per_gpu": S, "stripes_total": S_total,
             "parallelism": f"stripe-partitioned x{world} (no collectives on the data path)",
             "encode_bytes_per_step_per_gpu": enc_bytes,
             "repair_bytes_per_step_per_gpu": rep_bytes,

@@ -29,6 +29,23 @@ def stripe_shard(total: int, world: int, rank: int) -> tuple:
     return first, count
 
 
+def column_shard(block_bytes: int, world: int, rank: int, align: int = 4096) -> tuple:
+    """Byte-column share of every block for `rank` (SURVEY §8e fallback when a
+    batch has fewer stripes than GPUs): every byte column of a stripe is
+    independent, so rank i encodes/repairs columns [offset, offset + length)
+    of all blocks. Slices are multiples of `align` (the kernels' 4 KiB column
+    tile) except the last; returns (offset, length), length 0 for ranks past
+    the end."""
+    if world < 1 or not 0 <= rank < world or block_bytes < 0 or align < 1:
+        raise ValueError("bad shard request")
+    units = -(-block_bytes // align)
+    base, extra = divmod(units, world)
+    first = rank * base + min(rank, extra)
+    count = base + (1 if rank < extra else 0)
+    off = min(first * align, block_bytes)
+    return off, min((first + count) * align, block_bytes) - off
+
+
 def weak_shard(per_rank: int, rank: int) -> tuple:
     """Weak scaling: every rank owns `per_rank` stripes with distinct ids."""
     return rank * per_rank, per_rank

@@ -119,6 +119,32 @@ def test_encode_device_api_layouts(E, torch, orc, layout):
         assert not pbuf[:, B:].ne(0x5A).any(), "wrote past the block"
 
 
+def test_column_slices_match_full_encode(E, torch, orc):
+    """SURVEY §8e fallback: each "rank" encodes its column_shard slice of
+    every block (device pointers into the same blocks); together the slices
+    equal the whole-block encode, ragged last slice included."""
+    from ecwide_amd.shard import column_shard
+
+    k, m, r, B = 32, 3, 11, 5 * 4096 + 200
+    data = [orc.fill(B, 23, 0, j) for j in range(k)]
+    want = orc.codec("C", k, m, r, B).encode(data, threads=8)
+    stride = (B + 255) // 256 * 256  # device pointers must be 16-byte aligned
+    dbuf = torch.zeros((k, stride), dtype=torch.uint8, device="cuda")
+    for j in range(k):
+        dbuf[j, :B].copy_(torch.from_numpy(data[j]))
+    for world in (2, 3, 8):
+        pbuf = torch.zeros((len(want), stride), dtype=torch.uint8, device="cuda")
+        for rank in range(world):
+            off, n = column_shard(B, world, rank)
+            if n == 0:
+                continue
+            c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, n), 1, False)
+            c.encodeData([dbuf[j, off:off + n] for j in range(k)], [pbuf[i, off:off + n] for i in range(len(want))])
+        torch.cuda.synchronize()
+        for i, w in enumerate(want):
+            assert np.array_equal(pbuf[i, :B].cpu().numpy(), w), (world, i)
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]

@@ -6,3 +6,5 @@ timeout -k 10 400 $R --master-port 29533 bench.py --gpus 2 --steps 5 --warmup 1 
 tail -1 gpurun_out/bench_2rank.log | cut -c1-400
 timeout -k 10 400 $R --master-port 29534 bench.py --gpus 2 --steps 5 --warmup 1 --stripes 3 --strong > gpurun_out/bench_2rank_strong.log 2>&1 || exit $?
 tail -1 gpurun_out/bench_2rank_strong.log | cut -c1-600
+timeout -k 10 400 $R --master-port 29535 bench.py --gpus 2 --steps 5 --warmup 1 --stripes 1 --strong > gpurun_out/bench_2rank_columns.log 2>&1 || exit $?
+tail -1 gpurun_out/bench_2rank_columns.log | cut -c1-700
