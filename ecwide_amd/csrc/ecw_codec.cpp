@@ -125,7 +125,9 @@ struct ecw_codec {
     if (h_stage) (void)hipHostFree(h_stage);
     h_stage = nullptr;
     h_stage_bytes = 0;
-    if (hipHostMalloc(reinterpret_cast<void**>(&h_stage), bytes, hipHostMallocDefault) != hipSuccess)
+    // coherent: the zero-copy path (encode_stripes_packed) has kernels read and
+    // write this memory directly
+    if (hipHostMalloc(reinterpret_cast<void**>(&h_stage), bytes, hipHostMallocCoherent) != hipSuccess)
       return ECW_ENOMEM;
     h_stage_bytes = bytes;
     return ECW_OK;
@@ -793,6 +795,17 @@ namespace {
 // staging slots: the CPU packs batch b+1 (and unpacks batch b-1) while the
 // GPU copies and encodes batch b.
 constexpr size_t kPackBytes = size_t(32) << 20;  // host + device slot size
+// A batch whose packed image is at most this many bytes skips both copies:
+// the kernel reads the pinned image over PCIe and writes the parities back
+// into it (zero-copy). For a handful of 4 KiB stripes the two DMA transfers
+// are most of the round trip. ECW_ZERO_COPY_BYTES overrides (0 = off).
+size_t zero_copy_bytes() {
+  static const size_t v = [] {
+    const char* e = std::getenv("ECW_ZERO_COPY_BYTES");
+    return e ? static_cast<size_t>(std::strtoull(e, nullptr, 10)) : size_t(1) << 20;
+  }();
+  return v;
+}
 
 void copy_blocks(size_t n, size_t len, const std::function<void(size_t, size_t)>& fn) {
   // parallel memcpy loop for big batches only: a thread costs tens of us to
@@ -815,6 +828,23 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
   const size_t slot = sb_bytes * per;
   int st;
   if ((st = c->ensure_stage(slot * 2)) || (st = c->ensure_host_stage(slot * 2))) return st;
+  if (per >= stripes && sb_bytes * stripes <= zero_copy_bytes()) {
+    uint8_t* h = c->h_stage;
+    copy_blocks(static_cast<size_t>(stripes) * k, len, [&](size_t a, size_t e) {
+      for (size_t x = a; x < e; ++x) std::memcpy(h + (x / k) * sb_bytes + (x % k) * cs, data[x], len);
+    });
+    void* dp = nullptr;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return ECW_EDEVICE;
+    const SlabRows slab = slab_rows(static_cast<uint8_t*>(dp), cs, sb_bytes, k);
+    EncodeTarget t;
+    t.slab = &slab;
+    t.stripes = stripes;
+    if ((st = run_encode(c, t, len, P.s_run))) return st;
+    if (hipStreamSynchronize(P.s_run) != hipSuccess) return ECW_EDEVICE;
+    for (size_t x = 0; x < static_cast<size_t>(stripes) * np; ++x)
+      std::memcpy(parity[x], h + (x / np) * sb_bytes + (k + x % np) * cs, len);
+    return ECW_OK;
+  }
   int first[2] = {-1, -1}, count[2] = {0, 0};  // batch held by each slot, awaiting unpack
   auto unpack = [&](int q) -> int {
     if (first[q] < 0) return ECW_OK;
