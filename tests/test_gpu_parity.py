@@ -407,6 +407,40 @@ def test_linearity_full_size(E, torch):
         assert torch.equal(slab.parity(2)[i], slab.parity(0)[i] ^ slab.parity(1)[i]), i
 
 
+def test_max_block_size_1GiB(E, torch, orc):
+    """The reference's largest chunkSize (int lengths, powers of two <= 2^30,
+    SURVEY §8b) at k=128: 137 GiB of HBM. Column windows at the start, the
+    middle (odd offset) and the very end of every block vs the oracle on the
+    same window (columns are independent), every L block and D0 rebuilt
+    exactly over the whole GiB."""
+    k, m, r, B = 128, 3, 27, 1 << 30
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=1, block_bytes=B)
+    slab.fill_random(seed=77)
+    slab.encode()
+    out = torch.empty(B, dtype=torch.uint8, device="cuda")
+    slab.repair(0, out)
+    torch.cuda.synchronize()
+    assert torch.equal(out, slab.block(0, 0))
+    W = 1 << 16
+    oc = orc.codec("C", k, m, r, W)
+    par = slab.parity(0)
+    for off in (0, B // 2 + 7 * 4096 + 16, B - W):
+        data = [slab.block(0, j)[off:off + W].cpu().numpy() for j in range(k)]
+        want = oc.encode(data, threads=8)
+        for i, w in enumerate(want):
+            assert np.array_equal(par[i][off:off + W].cpu().numpy(), w), (off, i)
+    # local parities over the whole block: XOR of each group equals its L
+    g = c.groupNum
+    for t in range(g):
+        acc = torch.zeros(B, dtype=torch.uint8, device="cuda")
+        for j in range(t * r, min(k, (t + 1) * r)):
+            acc ^= slab.block(0, j)
+        assert torch.equal(acc, par[m + t]), t
+    del slab, out, acc
+    torch.cuda.empty_cache()
+
+
 def test_errors_are_loud(E, torch):
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(4, 2, 2, 4096), 1, False)
     base = torch.zeros(4096 * 8 + 64, dtype=torch.uint8, device="cuda")
