@@ -78,7 +78,7 @@ __global__ __launch_bounds__(256) void rows_lds_kernel(const uint8_t* base, uint
 // SM: 0 nontemporal stores into the stripe's 8 output rows, 1 plain stores
 // there, 2 nontemporal stores into one contiguous 32 KiB run per tile of a
 // separate buffer (out)
-template <bool ST, bool PF, int SM = 0>
+template <bool ST, bool PF, int SM = 0, int NST = 8>
 __global__ __launch_bounds__(256) void rows_st_kernel(uint8_t* base, uint64_t bstride, uint64_t sstride, int k,
                                                       uint64_t tiles_per_stripe, uint64_t ntiles, uint32_t* sink,
                                                       uint8_t* out = nullptr) {
@@ -110,7 +110,7 @@ __global__ __launch_bounds__(256) void rows_st_kernel(uint8_t* base, uint64_t bs
     }
     if (ST) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < NST; ++i) {
         if (SM == 0)
           __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(const_cast<uint8_t*>(p) + (uint64_t)(k + i) * bstride));
         else if (SM == 1)
@@ -136,6 +136,89 @@ __global__ __launch_bounds__(256) void rows_st_kernel(uint8_t* base, uint64_t bs
     u32x4 x = acc[0] ^ acc[1] ^ acc[2] ^ acc[3] ^ acc[4] ^ acc[5] ^ acc[6] ^ acc[7];
     if ((x.x ^ x.y ^ x.z ^ x.w) == 0x12345678u) sink[threadIdx.x] = 1;
   }
+}
+
+// Same bytes as rows_st<true,false,0,8>, but the 4 reading waves hand their 8
+// output rows to a 5th (writer) wave through LDS, so no reading wave ever
+// has a store outstanding (vmcnt is in order: a load issued after a store
+// cannot be consumed before the store is acknowledged).
+__global__ __launch_bounds__(320) void rows_wr_kernel(uint8_t* base, uint64_t bstride, uint64_t sstride, int k,
+                                                      uint64_t tiles_per_stripe, uint64_t ntiles, uint32_t* sink) {
+  __shared__ u32x4 stage[8][256];  // 32 KiB: [output row][lane of the 4 reading waves]
+  const int tid = threadIdx.x;
+  const bool writer = tid >= 256;
+  auto rowp = [&](uint64_t t, int j, int lane) {
+    const uint64_t s = t / tiles_per_stripe, c = t % tiles_per_stripe;
+    return base + s * sstride + c * 4096 + lane * 16 + (uint64_t)j * bstride;
+  };
+  if (writer) {
+    const int l = tid - 256;  // 64 writer lanes cover the 4 KiB tile row in 4 steps
+    for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+      __syncthreads();  // A: previous stage consumed (by us)
+      __syncthreads();  // B: stage holds this tile
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+          __builtin_nontemporal_store(stage[i][q * 64 + l],
+                                      reinterpret_cast<u32x4*>(rowp(tile, k + i, q * 64 + l)));
+    }
+    return;
+  }
+  u32x4 acc[8];
+  uint64_t tile = blockIdx.x;
+  if (tile >= ntiles) return;  // grid <= ntiles on the host side, so never taken
+  u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowp(tile, 0, tid)));
+  u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowp(tile, 1, tid)));
+  for (; tile < ntiles; tile += gridDim.x) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = u32x4{0, 0, 0, 0};
+    const uint8_t* p = rowp(tile, 0, tid);
+    for (int j = 0; j < k - 2; j += 2) {
+      acc[j & 7] ^= a;
+      a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (uint64_t)(j + 2) * bstride));
+      acc[(j + 1) & 7] ^= b;
+      b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (uint64_t)(j + 3) * bstride));
+    }
+    acc[6] ^= a;
+    acc[7] ^= b;
+    const uint64_t nt = tile + gridDim.x;
+    if (nt < ntiles) {
+      a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowp(nt, 0, tid)));
+      b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(rowp(nt, 1, tid)));
+    }
+    __syncthreads();  // A
+#pragma unroll
+    for (int i = 0; i < 8; ++i) stage[i][tid] = acc[i];
+    __syncthreads();  // B
+  }
+}
+
+// flat reads (each tile's 128 x 4 KiB contiguous) + NST output rows into a
+// separate contiguous region; and a plain 16 B/lane copy
+template <int NST, bool INPLACE = false>
+__global__ __launch_bounds__(256) void flat_st_kernel(const uint8_t* in, uint8_t* out, int k, uint64_t ntiles) {
+  u32x4 acc[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = u32x4{0, 0, 0, 0};
+  for (uint64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const uint8_t* p = in + tile * (INPLACE ? k + 8 : k) * 4096 + threadIdx.x * 16;
+    for (int j = 0; j < k; j += 2) {
+      u32x4 a = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (uint64_t)j * 4096));
+      u32x4 b = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p + (uint64_t)(j + 1) * 4096));
+      acc[j & 7] ^= a;
+      acc[(j + 1) & 7] ^= b;
+    }
+#pragma unroll
+    for (int i = 0; i < NST; ++i)
+      __builtin_nontemporal_store(acc[i], reinterpret_cast<u32x4*>(
+          INPLACE ? const_cast<uint8_t*>(p) + (uint64_t)(k + i) * 4096 : out + (tile * NST + i) * 4096 + threadIdx.x * 16));
+  }
+}
+
+__global__ __launch_bounds__(256) void copy_kernel(const u32x4* in, u32x4* out, uint64_t n) {
+  for (uint64_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += gridDim.x * 256ull)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(in + i), out + i);
 }
 
 __global__ void fill_random(uint64_t* p, uint64_t n) {
@@ -213,6 +296,47 @@ int main(int argc, char** argv) {
     const unsigned grid = GRID ? GRID : (unsigned)ntiles;                                                    \
     double ms = time_ms([&] { rows_st_kernel<true, false, SM><<<grid, 256>>>(buf, bstride, sstride, k, tps, ntiles, sink, out); }, iters); \
     std::printf("rows_st sm=%d grid=%u  %8.1f GB/s (136 rows counted)\n", SM, grid, sbytes / ms / 1e6);     \
+  }
+#define RSN(NST)                                                                                             \
+  {                                                                                                          \
+    double ms = time_ms([&] { rows_st_kernel<true, false, 0, NST><<<65536, 256>>>(buf, bstride, sstride, k, tps, ntiles, sink, out); }, iters); \
+    const double by = (double)S * (k + NST) * B;                                                             \
+    std::printf("rows_st stores=%d grid=65536  %8.1f GB/s (128+%d rows counted)\n", NST, by / ms / 1e6, NST);  \
+  }
+  if (argc > 6) {
+    const uint64_t n16 = (uint64_t)S * k * B / 16 / 2;
+    for (int rep = 0; rep < 2; ++rep) {
+      for (unsigned grid : {65536u, 262144u}) {
+        double ms = time_ms([&] { copy_kernel<<<grid, 256>>>(reinterpret_cast<const u32x4*>(buf),
+                                                             reinterpret_cast<u32x4*>(buf) + n16, n16); }, iters);
+        std::printf("copy grid=%u  %8.1f GB/s (read + write)\n", grid, 2.0 * n16 * 16 / ms / 1e6);
+      }
+#define FST(NST)                                                                                             \
+  {                                                                                                          \
+    double ms = time_ms([&] { flat_st_kernel<NST><<<65536, 256>>>(buf, out, k, ntiles); }, iters);           \
+    std::printf("flat_st stores=%d  %8.1f GB/s (128+%d rows counted)\n", NST, (double)S * (k + NST) * B / ms / 1e6, NST); \
+  }
+      FST(1) FST(8)
+      {
+        double ms = time_ms([&] { flat_st_kernel<8, true><<<65536, 256>>>(buf, out, k, ntiles); }, iters);
+        std::printf("flat_st in-place (4 KiB chunk layout) stores=8  %8.1f GB/s (136 rows counted)\n", (double)S * (k + 8) * B / ms / 1e6);
+      }
+      for (unsigned grid : {65536u, 131072u}) {
+        double ms = time_ms([&] { rows_st_kernel<true, false, 0, 8><<<grid, 256>>>(buf, bstride, sstride, k, tps, ntiles, sink, out); }, iters);
+        std::printf("rows_st stores=8 grid=%u  %8.1f GB/s (136 rows counted)\n", grid, (double)S * (k + 8) * B / ms / 1e6);
+      }
+    }
+    return 0;
+  }
+  if (argc > 5) {
+    for (int rep = 0; rep < 2; ++rep) {
+      RS(false, false, 65536) RSN(1) RSN(8)
+      for (unsigned grid : {16384u, 32768u, 65536u}) {
+        double ms = time_ms([&] { rows_wr_kernel<<<grid, 320>>>(buf, bstride, sstride, k, tps, ntiles, sink); }, iters);
+        std::printf("rows_wr (writer wave) grid=%u  %8.1f GB/s (136 rows counted)\n", grid, sbytes / ms / 1e6);
+      }
+    }
+    return 0;
   }
   for (int rep = 0; rep < 2; ++rep) {
     RSM(0, 65536) RSM(1, 65536) RSM(3, 65536) RSM(4, 65536) RSM(5, 65536) RSM(6, 65536) RSM(7, 65536)
