@@ -286,7 +286,10 @@ template <int NW, int P, int LOCAL, class Rows>
 #ifndef ECW_ENC_MIN_WAVES
 #define ECW_ENC_MIN_WAVES 6  // __launch_bounds__ min waves per SIMD: caps VGPRs at 80 (+1-4 %; spills only outside the row loop)
 #endif
-__global__ __launch_bounds__(kBlock, ECW_ENC_MIN_WAVES) void encode_kernel(const Rows rows, const EncodeGeom g,
+#ifndef ECW_ENC_MIN_WAVES_NW2
+#define ECW_ENC_MIN_WAVES_NW2 4  // 5-8 rows: 128 VGPRs (at 80 the 32 accumulators spill inside the row loop)
+#endif
+__global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ENC_MIN_WAVES : ECW_ENC_MIN_WAVES_NW2) void encode_kernel(const Rows rows, const EncodeGeom g,
                                                         const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // workgroup b takes tiles begin + b, + grid, + 2 grid, ... (concurrently
