@@ -564,8 +564,17 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
   if (total == 0) return hipSuccess;
   if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), dim3(grid_for(total, ECW_GRID_PER_CU_XOR)), dim3(kBlock), 0,
-                     s, a, g);
+  // ring depth <= n: the ring refills past the last row re-read row n-1, so a
+  // depth-8 ring over 1-2 sources would load every byte up to 8 times
+  const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR)), block(kBlock);
+  if (g.n <= 1)
+    hipLaunchKernelGGL((xor_kernel<1, Args>), grid, block, 0, s, a, g);
+  else if (g.n <= 2)
+    hipLaunchKernelGGL((xor_kernel<2, Args>), grid, block, 0, s, a, g);
+  else if (g.n <= 4)
+    hipLaunchKernelGGL((xor_kernel<4, Args>), grid, block, 0, s, a, g);
+  else
+    hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), grid, block, 0, s, a, g);
   return hipGetLastError();
 }
 
