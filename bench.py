@@ -47,6 +47,8 @@ def parse():
     ap.add_argument("--strong", action="store_true",
                     help="strong scaling (BASELINE configs[4]): --stripes (or the --hbm-fill batch) is the "
                          "TOTAL, split by stripe across the ranks")
+    ap.add_argument("--pageable", action="store_true",
+                    help="with --host-resident: ordinary pageable host blocks instead of pinned ones")
     ap.add_argument("--host-resident", action="store_true",
                     help="measure the PCIe-inclusive rate (pinned host blocks) instead")
     return ap.parse_args()
@@ -165,7 +167,7 @@ def host_resident(args):
     B = int(args.block_mib * (1 << 20))
     codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
     nblk = k + codec.parityNum
-    hb = torch.empty(nblk * B, dtype=torch.uint8, pin_memory=True)
+    hb = torch.empty(nblk * B, dtype=torch.uint8, pin_memory=not args.pageable)
     slab = E.StripeSlab(codec, stripes=1, block_bytes=B)
     slab.fill_random(seed=args.seed)
     for j in range(k):
@@ -173,7 +175,7 @@ def host_resident(args):
     del slab
     torch.cuda.synchronize()
     views = [hb[i * B:(i + 1) * B].numpy() for i in range(nblk)]
-    out = torch.empty(B, dtype=torch.uint8, pin_memory=True).numpy()
+    out = torch.empty(B, dtype=torch.uint8, pin_memory=not args.pageable).numpy()
     enc_b = nblk * B
     rep_b = (len(codec.repairSources(0)) + 1) * B
     codec.encodeData(views[:k], views[k:])
@@ -188,7 +190,9 @@ def host_resident(args):
     t2 = time.perf_counter()
     assert np.array_equal(out, views[0])
     line = {
-        "metric": "host-resident encode + single-block-repair GB/s (pinned host blocks, hipMemcpyAsync in/out)",
+        "metric": ("host-resident encode + single-block-repair GB/s "
+                   + ("(pageable host blocks, e.g. Java direct ByteBuffers)" if args.pageable
+                      else "(pinned host blocks, hipMemcpyAsync in/out)")),
         "value": round(it * (enc_b + rep_b) / (t2 - t0) / 1e9, 2),
         "unit": "GB/s", "n_gpus": 1, "iters": it,
         "encode_GBps": round(it * enc_b / (t1 - t0) / 1e9, 2),
