@@ -1,5 +1,6 @@
 // Hand-scheduled encode of ONE full column tile (gfx950 / CDNA4), used by
-// encode_kernel_asm for every encode pass with <= 4 global rows (slab or pointer mode).
+// encode_kernel_asm for every encode pass (slab or pointer mode; <= 4 global rows
+// below, 5-8 rows in the ECW2_* variant further down).
 //
 // Same arithmetic as encode_tile() in ecw_kernels.hip (ISA-L's 4-bit split
 // GF(2^8) products, gf_vect_mul_init, isal:erasure_code/ec_base.c:157-262,
@@ -345,6 +346,217 @@
   ECW_TILE_OPERANDS, "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67", "v68", \
     "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77"
 
+// ---------------------------------------------------------------------------
+// 5-8 global rows (NW = 2): the same tile with one u64 table entry per nibble
+// (rows 0-3 in the low dword, 4-7 in the high one; records of 256 B, lo-nibble
+// entries at +0, hi at +128) and a second bank of packed accumulators.
+// Registers as above except: v33 = 0x78787878 (nibble * 8), lookup sets
+// v[42:57] / v[58:73] (eight even-aligned pairs each, the address in the low
+// register of its pair), accumulators of rows 4-7 in v[74:89], parked local
+// parities in v[90:109].
+#define ECW2_DW_ADDR(W, A0, A1, A2, A3, A4, A5, A6, A7) \
+  "v_lshlrev_b32 v34, 3, " W "\n\t"                     \
+  "v_lshrrev_b32 v35, 1, " W "\n\t"                     \
+  "v_and_or_b32 v34, v34, v33, s48\n\t"                 \
+  "v_and_or_b32 v35, v35, v33, s48\n\t"                 \
+  "v_perm_b32 " A0 ", v32, v34, s50\n\t"                \
+  "v_perm_b32 " A1 ", v32, v35, s50\n\t"                \
+  "v_perm_b32 " A2 ", v32, v34, s51\n\t"                \
+  "v_perm_b32 " A3 ", v32, v35, s51\n\t"                \
+  "v_perm_b32 " A4 ", v32, v34, s52\n\t"                \
+  "v_perm_b32 " A5 ", v32, v35, s52\n\t"                \
+  "v_perm_b32 " A6 ", v32, v34, s53\n\t"                \
+  "v_perm_b32 " A7 ", v32, v35, s53\n\t"
+#define ECW2_ADDR_X(W) ECW2_DW_ADDR(W, "v42", "v44", "v46", "v48", "v50", "v52", "v54", "v56")
+#define ECW2_ADDR_Y(W) ECW2_DW_ADDR(W, "v58", "v60", "v62", "v64", "v66", "v68", "v70", "v72")
+#define ECW2_READ_X                                 \
+  "ds_read_b64 v[42:43], v42\n\t"                   \
+  "ds_read_b64 v[44:45], v44 offset:128\n\t"        \
+  "ds_read_b64 v[46:47], v46\n\t"                   \
+  "ds_read_b64 v[48:49], v48 offset:128\n\t"        \
+  "ds_read_b64 v[50:51], v50\n\t"                   \
+  "ds_read_b64 v[52:53], v52 offset:128\n\t"        \
+  "ds_read_b64 v[54:55], v54\n\t"                   \
+  "ds_read_b64 v[56:57], v56 offset:128\n\t"
+#define ECW2_READ_Y                                 \
+  "ds_read_b64 v[58:59], v58\n\t"                   \
+  "ds_read_b64 v[60:61], v60 offset:128\n\t"        \
+  "ds_read_b64 v[62:63], v62\n\t"                   \
+  "ds_read_b64 v[64:65], v64 offset:128\n\t"        \
+  "ds_read_b64 v[66:67], v66\n\t"                   \
+  "ds_read_b64 v[68:69], v68 offset:128\n\t"        \
+  "ds_read_b64 v[70:71], v70\n\t"                   \
+  "ds_read_b64 v[72:73], v72 offset:128\n\t"
+// byte b of the dword: lo-nibble pair (L, L+1), hi-nibble pair (H, H+1) into
+// accumulators C (rows 0-3) and D (rows 4-7)
+#define ECW2_FOLD1(C, D, L, L1, H, H1)                    \
+  "v_bitop3_b32 " C ", " C ", " L ", " H " bitop3:0x96\n\t"  \
+  "v_bitop3_b32 " D ", " D ", " L1 ", " H1 " bitop3:0x96\n\t"
+#define ECW2_FOLD_X(C0, C1, C2, C3, D0, D1, D2, D3)        \
+  ECW2_FOLD1(C0, D0, "v42", "v43", "v44", "v45")           \
+  ECW2_FOLD1(C1, D1, "v46", "v47", "v48", "v49")           \
+  ECW2_FOLD1(C2, D2, "v50", "v51", "v52", "v53")           \
+  ECW2_FOLD1(C3, D3, "v54", "v55", "v56", "v57")
+#define ECW2_FOLD_Y(C0, C1, C2, C3, D0, D1, D2, D3)        \
+  ECW2_FOLD1(C0, D0, "v58", "v59", "v60", "v61")           \
+  ECW2_FOLD1(C1, D1, "v62", "v63", "v64", "v65")           \
+  ECW2_FOLD1(C2, D2, "v66", "v67", "v68", "v69")           \
+  ECW2_FOLD1(C3, D3, "v70", "v71", "v72", "v73")
+#define ECW2_ROW(R0, R1, R2, R3, XL)                                                   \
+  "s_lshr_b32 s47, s46, 8\n\t"                                                         \
+  "s_and_b32 s48, s46, 0xff\n\t"                                                       \
+  "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
+  "v_mov_b32 v32, s47\n\t"                                                             \
+  ECW2_ADDR_X(R0) ECW2_READ_X                                                          \
+  ECW2_ADDR_Y(R1) ECW2_READ_Y                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_X("v12", "v13", "v14", "v15", "v74", "v75", "v76", "v77")                 \
+  ECW2_ADDR_X(R2) ECW2_READ_X                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_Y("v16", "v17", "v18", "v19", "v78", "v79", "v80", "v81")                 \
+  ECW2_ADDR_Y(R3) ECW2_READ_Y                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_X("v20", "v21", "v22", "v23", "v82", "v83", "v84", "v85")                 \
+  ECW_LACC_##XL(R0, R1, R2, R3)                                                        \
+  "s_waitcnt lgkmcnt(0)\n\t"                                                           \
+  ECW2_FOLD_Y("v24", "v25", "v26", "v27", "v86", "v87", "v88", "v89")                 \
+  "s_add_u32 s46, s46, 256\n\t"
+#define ECW2_ROW_A(XL) ECW2_ROW("v4", "v5", "v6", "v7", XL)
+#define ECW2_ROW_B(XL) ECW2_ROW("v8", "v9", "v10", "v11", XL)
+
+#define ECW2_BOUNDARY_PARK                                  \
+  "s_add_u32 s49, s44, 1\n\t"                               \
+  "s_cmp_eq_u32 s49, s45\n\t"                               \
+  "s_cbranch_scc0 20f\n\t"                                  \
+  ECW_PARK(0, "v90", "v91", "v92", "v93", 21)               \
+  ECW_PARK(1, "v94", "v95", "v96", "v97", 22)               \
+  ECW_PARK(2, "v98", "v99", "v100", "v101", 23)             \
+  ECW_PARK(3, "v102", "v103", "v104", "v105", 24)           \
+  ECW_PARK(4, "v106", "v107", "v108", "v109", 25)           \
+  "26:\n\t"                                                 \
+  "s_add_u32 s59, s59, 1\n\t"                               \
+  "s_add_u32 s45, s45, %[r]\n\t"                            \
+  "s_min_u32 s45, s45, %[k]\n\t"                            \
+  ECW_LRESET_1                                              \
+  "20:\n\t"
+#define ECW2_STORE_PARKED(MODE)                                             \
+  ECW_LPTR_INIT_##MODE                                                      \
+  ECW_UNPARK(0, "v[90:93]", MODE) ECW_UNPARK(1, "v[94:97]", MODE)           \
+  ECW_UNPARK(2, "v[98:101]", MODE) ECW_UNPARK(3, "v[102:105]", MODE)        \
+  ECW_UNPARK(4, "v[106:109]", MODE)                                         \
+  "27:\n\t"
+
+// byte s49 of the packed accumulators C0..C15 -> v[36:39] (selectors s57/s58)
+#define ECW2_TRANSPOSE(C0, C1, C2, C3, C4, C5, C6, C7, C8, C9, C10, C11, C12, C13, C14, C15) \
+  "v_perm_b32 v34, " C1 ", " C0 ", s57\n\t"                                 \
+  "v_perm_b32 v35, " C3 ", " C2 ", s58\n\t"                                 \
+  "v_or_b32 v36, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, " C5 ", " C4 ", s57\n\t"                                 \
+  "v_perm_b32 v35, " C7 ", " C6 ", s58\n\t"                                 \
+  "v_or_b32 v37, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, " C9 ", " C8 ", s57\n\t"                                 \
+  "v_perm_b32 v35, " C11 ", " C10 ", s58\n\t"                               \
+  "v_or_b32 v38, v34, v35\n\t"                                              \
+  "v_perm_b32 v34, " C13 ", " C12 ", s57\n\t"                               \
+  "v_perm_b32 v35, " C15 ", " C14 ", s58\n\t"                               \
+  "v_or_b32 v39, v34, v35\n\t"
+
+#define ECW2_TILE_ASM(BND, XL, END, MODE)                                          \
+  "v_mov_b32 v40, %[col]\n\t"                                               \
+  "v_mov_b32 v33, 0x78787878\n\t"                                           \
+  "s_mov_b32 s50, 0x0c0c0400\n\t"                                           \
+  "s_mov_b32 s51, 0x0c0c0401\n\t"                                           \
+  "s_mov_b32 s52, 0x0c0c0402\n\t"                                           \
+  "s_mov_b32 s53, 0x0c0c0403\n\t"                                           \
+  ECW_ROWPTR_INIT_##MODE                                                    \
+  ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
+  ECW_LOAD_B ECW_NEXTROW_##MODE                                             \
+  "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
+  "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
+  "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
+  "v_mov_b32 v24, 0\n\tv_mov_b32 v25, 0\n\tv_mov_b32 v26, 0\n\tv_mov_b32 v27, 0\n\t" \
+  "v_mov_b32 v74, 0\n\tv_mov_b32 v75, 0\n\tv_mov_b32 v76, 0\n\tv_mov_b32 v77, 0\n\t" \
+  "v_mov_b32 v78, 0\n\tv_mov_b32 v79, 0\n\tv_mov_b32 v80, 0\n\tv_mov_b32 v81, 0\n\t" \
+  "v_mov_b32 v82, 0\n\tv_mov_b32 v83, 0\n\tv_mov_b32 v84, 0\n\tv_mov_b32 v85, 0\n\t" \
+  "v_mov_b32 v86, 0\n\tv_mov_b32 v87, 0\n\tv_mov_b32 v88, 0\n\tv_mov_b32 v89, 0\n\t" \
+  "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  "s_mov_b32 s44, 0\n\t"                                                    \
+  "s_mov_b32 s59, 0\n\t"                                                    \
+  "s_mov_b32 s46, %[lds]\n\t"                                               \
+  ECW_LPTR_INIT_##MODE                                                      \
+  "s_min_u32 s45, %[r], %[k]\n\t"                                           \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 3\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW2_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW_##MODE                          \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW2_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW_##MODE                          \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc0 12f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW2_ROW_A(XL) BND ECW_LOAD_A                                             \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW2_ROW_B(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW2_ROW_A(XL) BND                                                        \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW2_ROW_A(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW2_ROW_B(XL) BND                                                        \
+  "13:\n\t"                                                                 \
+  END                                                                       \
+  /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \
+  ECW_GPTR_INIT_##MODE                                                      \
+  "s_mov_b32 s56, 0\n\t"                                                    \
+  "30:\n\t"                                                                 \
+  "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
+  "s_cbranch_scc1 31f\n\t"                                                  \
+  "s_and_b32 s49, s56, 3\n\t"                                               \
+  "s_add_u32 s57, s49, 4\n\t"                                               \
+  "s_lshl_b32 s58, s57, 24\n\t"                                             \
+  "s_lshl_b32 s57, s57, 8\n\t"                                              \
+  "s_or_b32 s57, s57, s49\n\t"                                              \
+  "s_or_b32 s57, s57, 0x0c0c0000\n\t"                                       \
+  "s_lshl_b32 s49, s49, 16\n\t"                                             \
+  "s_or_b32 s58, s58, s49\n\t"                                              \
+  "s_or_b32 s58, s58, 0x0c0c\n\t"                                           \
+  "s_cmp_ge_u32 s56, 4\n\t"                                                 \
+  "s_cbranch_scc1 32f\n\t"                                                  \
+  ECW2_TRANSPOSE("v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19",    \
+                 "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27")    \
+  "s_branch 33f\n\t"                                                        \
+  "32:\n\t"                                                                 \
+  ECW2_TRANSPOSE("v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81",    \
+                 "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89")    \
+  "33:\n\t"                                                                 \
+  ECW_GPTR_GET_##MODE                                                       \
+  ECW_ASM_GSTORE("v[36:39]", "s[54:55]")                                    \
+  "s_nop 1\n\t"                                                             \
+  ECW_GPTR_NEXT_##MODE                                                      \
+  "s_add_u32 s56, s56, 1\n\t"                                               \
+  "s_branch 30b\n\t"                                                        \
+  "31:"
+
+#define ECW2_TILE_OPERANDS                                                          \
+  ECW_TILE_OPERANDS, "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67",  \
+    "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80",      \
+    "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89"
+#define ECW2_TILE_OPERANDS_PARK                                                     \
+  ECW2_TILE_OPERANDS, "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",       \
+    "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109"
+
 namespace ecw {
 namespace {
 
@@ -366,11 +578,31 @@ namespace {
                      ECW_TILE_OPERANDS);                                                 \
   }
 
-template <int LOCAL, bool PARK, bool TAB>
+#define ECW2_TILE_CALL(MODE)                                                             \
+  if constexpr (LOCAL == kLocalNone) {                                                   \
+    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW2_TILE_OPERANDS);         \
+  } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
+    asm volatile(ECW2_TILE_ASM(ECW2_BOUNDARY_PARK, 1, ECW2_STORE_PARKED(MODE), MODE)     \
+                     ECW2_TILE_OPERANDS_PARK);                                           \
+  } else if constexpr (LOCAL == kLocalXor) {                                             \
+    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW2_TILE_OPERANDS);     \
+  } else {                                                                               \
+    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
+                     ECW2_TILE_OPERANDS);                                                \
+  }
+
+// NW = 1: <= 4 global rows (u32 table entries); NW = 2: 5-8 rows (u64 entries)
+template <int LOCAL, bool PARK, bool TAB, int NW = 1>
 __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
                                                 int k, int r, int nrows, uint32_t lds, uint32_t col) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
-  if constexpr (TAB) {
+  if constexpr (NW == 2) {
+    if constexpr (TAB) {
+      ECW2_TILE_CALL(TAB)
+    } else {
+      ECW2_TILE_CALL(SLAB)
+    }
+  } else if constexpr (TAB) {
     ECW_TILE_CALL(TAB)
   } else {
     ECW_TILE_CALL(SLAB)

@@ -355,11 +355,15 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 // arguments: `rows` is the first argument, so it sits at offset 0 of the
 // kernarg segment (taking the address of the by-value argument itself
 // would make the compiler copy all 3 KiB of it to scratch).
-template <int LOCAL, bool PARK, class Rows>
-__global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_asm(const Rows rows, const EncodeGeom g,
-                                                                              const uint4* __restrict__ tbl) {
+#ifndef ECW_ASM_MIN_WAVES_NW2
+#define ECW_ASM_MIN_WAVES_NW2 4  // 128 VGPRs: the 8-row tile uses 110
+#endif
+
+template <int LOCAL, bool PARK, class Rows, int NW = 1>
+__global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_WAVES_NW2) void encode_kernel_asm(
+    const Rows rows, const EncodeGeom g, const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int n16 = g.k * 8;
+  const int n16 = g.k * 8 * NW;
   for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
   __syncthreads();
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
@@ -374,14 +378,14 @@ __global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_asm(c
         const uint64_t so = static_cast<uint64_t>(cur.s) * rows.sstride;
         const uint8_t* sb = uniform_ptr(rows.base + so);
         const uint8_t* pb = uniform_ptr(rows.pbase + so);
-        encode_tile_asm<LOCAL, PARK, false>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
+        encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
                                             const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * bs), bs, k, r,
                                             nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
       } else {
         const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
             reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
         const uint8_t* dtab = ka + offsetof(PtrRows, dst);
-        encode_tile_asm<LOCAL, PARK, true>(ka + offsetof(PtrRows, src),
+        encode_tile_asm<LOCAL, PARK, true, NW>(ka + offsetof(PtrRows, src),
                                            const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
                                            const_cast<uint8_t*>(dtab), 0, k, r, nrows,
                                            __builtin_amdgcn_readfirstlane(lds_base), cur.col);
@@ -389,7 +393,7 @@ __global__ __launch_bounds__(kBlock, ECW_ASM_MIN_WAVES) void encode_kernel_asm(c
     } else {
       uint4 ring[kPrefetchEncAsmTail];
       ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
-      encode_tile<1, kPrefetchEncAsmTail, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
+      encode_tile<NW, kPrefetchEncAsmTail, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
     }
   }
 }
@@ -512,21 +516,21 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
   return hipGetLastError();
 }
 
-template <class Rows>
+template <class Rows, int NW>
 hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
-  const size_t lds = static_cast<size_t>(g.k) * 128;
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
   switch (g.local_mode) {
     case kLocalXor:
       if (g.groups <= kMaxParkedLocals)
-        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, true, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, true, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       else
-        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      hipLaunchKernelGGL((encode_kernel_asm<kLocalZero, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      hipLaunchKernelGGL((encode_kernel_asm<kLocalZero, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
       break;
     default:
-      hipLaunchKernelGGL((encode_kernel_asm<kLocalNone, false, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      hipLaunchKernelGGL((encode_kernel_asm<kLocalNone, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
   }
   return hipGetLastError();
 }
@@ -548,8 +552,9 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
     g.tile_end = t0 + win < total ? t0 + win : total;
     const dim3 grid(grid_for(g.tile_end - g.tile_begin));
     hipError_t e;
-    if (ECW_ENC_ASM && g.nrows <= 4 && g.k >= 2) {
-      e = launch_encode_asm(rows, g, tbl, grid, s);
+    if (ECW_ENC_ASM && g.k >= 2) {
+      e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+                       : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
       if (e != hipSuccess) return e;
       continue;
     }

@@ -224,7 +224,10 @@ def test_fill_kernel_matches_oracle(E, torch, orc):
                                        # asm tile (slab, <= 4 global rows): odd k (3-row epilogue), the
                                        # minimum k = 2, one group, > 5 groups (stores not parked)
                                        (33, 3, 4, 3 * 4096 + 100, 2), (31, 4, 31, 8192, 2), (2, 1, 1, 8192, 3),
-                                       (3, 2, 2, 8192, 2), (128, 3, 8, 1 << 16, 2), (6, 4, 1, 4096, 2)])
+                                       (3, 2, 2, 8192, 2), (128, 3, 8, 1 << 16, 2), (6, 4, 1, 4096, 2),
+                                       # the 5-8-row asm tile: parked (<= 5 groups) and not, k = 2 / 3
+                                       (128, 6, 27, 1 << 16, 2), (40, 8, 7, 3 * 4096 + 48, 2),
+                                       (3, 7, 2, 8192, 2), (2, 5, 1, 4096, 2)])
 def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S):
     """Batched slab encode vs oracle at mid sizes; repair of every data and
     local block of stripe 0 equals the erased block."""
@@ -257,9 +260,9 @@ def test_random_sweep_vs_oracle(E, torch, orc):
     in slab mode and in pointer mode (block j stored at slot k-1-j, so the
     pointers are not one stride apart)."""
     rng = np.random.default_rng(2026)
-    for trial in range(24):
+    for trial in range(32):
         k = int(rng.integers(2, 160))
-        m = int(rng.integers(1, 5))
+        m = int(rng.integers(1, 9))  # 1-4 rows: the u32-entry tile, 5-8: the u64-entry tile
         r = int(rng.integers(1, k + 1))
         B = int(rng.choice([4096, 8192, 4096 * int(rng.integers(1, 4)) + 16 * int(rng.integers(1, 256))]))
         S = int(rng.integers(1, 3))
@@ -343,7 +346,7 @@ def test_multinode_encode_chain(E, torch, orc, k, m, r, B):
         assert np.array_equal(chain[i].cpu().numpy(), want[i]), i
 
 
-@pytest.mark.parametrize("k,m,r", [(32, 2, 8), (33, 3, 4)])
+@pytest.mark.parametrize("k,m,r", [(32, 2, 8), (33, 3, 4), (128, 6, 27)])
 def test_literal_mode_slab_writes_zero_locals(E, torch, orc, k, m, r):
     """ECWide-C literal mode: every L block is written as zeros (parked and
     unparked asm paths); the global parities are unchanged."""
