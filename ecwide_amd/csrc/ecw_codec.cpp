@@ -74,7 +74,7 @@ struct ecw_codec {
   size_t h_stage_bytes = 0;
 
   ~ecw_codec() {
-    if (dev_ready) {
+    if (dev_ready || !d_pass.empty()) {
       DeviceGuard g(device);
       for (void* p : d_pass) (void)hipFree(p);
       if (d_stage) (void)hipFree(d_stage);
@@ -97,16 +97,18 @@ struct ecw_codec {
     if (dev_ready) return ECW_OK;
     DeviceGuard g(device);
     if (!g.ok) return ECW_EDEVICE;
+    auto fail = [&](int st) {  // leave nothing half-initialised: a later call retries from scratch
+      for (void* q : d_pass) (void)hipFree(q);
+      d_pass.clear();
+      return st;
+    };
     for (const auto& img : pass_img) {
       void* p = nullptr;
-      if (hipMalloc(&p, img.size()) != hipSuccess) return ECW_ENOMEM;
-      if (hipMemcpy(p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) {
-        (void)hipFree(p);
-        return ECW_EDEVICE;
-      }
+      if (hipMalloc(&p, img.size()) != hipSuccess) return fail(ECW_ENOMEM);
       d_pass.push_back(p);
+      if (hipMemcpy(p, img.data(), img.size(), hipMemcpyHostToDevice) != hipSuccess) return fail(ECW_EDEVICE);
     }
-    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return ECW_EDEVICE;
+    if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(ECW_EDEVICE);
     dev_ready = true;
     return ECW_OK;
   }
