@@ -692,6 +692,14 @@ struct HostPipe {
   }
 };
 
+// error exit of a pipelined call: let the copies already queued on the
+// pipeline's streams finish before the caller may free its buffers
+static int drain(HostPipe& P, int st) {
+  for (hipStream_t x : {P.s_in, P.s_run, P.s_out})
+    if (x) (void)hipStreamSynchronize(x);
+  return st;
+}
+
 typedef int (*host_op)(ecw_codec*, uint8_t* const*, int, uint8_t* const*, int, size_t, hipStream_t);
 
 static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8_t* const* out, int nout,
@@ -724,19 +732,19 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
     uint8_t* base = c->d_stage + slot * slot_bytes;
     for (int b = 0; b < nin; ++b) din[b] = base + b * cstride;
     for (int b = 0; b < nout; ++b) dout[b] = base + (nin + b) * cstride;
-    if (i >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return ECW_EDEVICE;
+    if (i >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
     for (int b = 0; b < nin; ++b)
-      if (hipMemcpyAsync(din[b], in[b] + c0, n, hipMemcpyHostToDevice, P.s_in) != hipSuccess) return ECW_EDEVICE;
-    if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return ECW_EDEVICE;
-    if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return ECW_EDEVICE;
-    if ((st = op(c, din.data(), nin, dout.data(), nout, n, P.s_run))) return st;
-    if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return ECW_EDEVICE;
-    if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      if (hipMemcpyAsync(din[b], in[b] + c0, n, hipMemcpyHostToDevice, P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if ((st = op(c, din.data(), nin, dout.data(), nout, n, P.s_run))) return drain(P, st);
+    if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
     for (int b = 0; b < nout; ++b)
-      if (hipMemcpyAsync(out[b] + c0, dout[b], n, hipMemcpyDeviceToHost, P.s_out) != hipSuccess) return ECW_EDEVICE;
-    if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return ECW_EDEVICE;
+      if (hipMemcpyAsync(out[b] + c0, dout[b], n, hipMemcpyDeviceToHost, P.s_out) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return drain(P, ECW_EDEVICE);
   }
-  if (hipStreamSynchronize(P.s_out) != hipSuccess) return ECW_EDEVICE;
+  if (hipStreamSynchronize(P.s_out) != hipSuccess) return drain(P, ECW_EDEVICE);
   return hipStreamSynchronize(P.s_run) == hipSuccess ? ECW_OK : ECW_EDEVICE;
 }
 
@@ -836,13 +844,13 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
       for (size_t x = a; x < e; ++x) std::memcpy(h + (x / k) * sb_bytes + (x % k) * cs, data[x], len);
     });
     void* dp = nullptr;
-    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return ECW_EDEVICE;
+    if (hipHostGetDevicePointer(&dp, h, 0) != hipSuccess) return drain(P, ECW_EDEVICE);
     const SlabRows slab = slab_rows(static_cast<uint8_t*>(dp), cs, sb_bytes, k);
     EncodeTarget t;
     t.slab = &slab;
     t.stripes = stripes;
-    if ((st = run_encode(c, t, len, P.s_run))) return st;
-    if (hipStreamSynchronize(P.s_run) != hipSuccess) return ECW_EDEVICE;
+    if ((st = run_encode(c, t, len, P.s_run))) return drain(P, st);
+    if (hipStreamSynchronize(P.s_run) != hipSuccess) return drain(P, ECW_EDEVICE);
     for (size_t x = 0; x < static_cast<size_t>(stripes) * np; ++x)
       std::memcpy(parity[x], h + (x / np) * sb_bytes + (k + x % np) * cs, len);
     return ECW_OK;
@@ -850,7 +858,7 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
   int first[2] = {-1, -1}, count[2] = {0, 0};  // batch held by each slot, awaiting unpack
   auto unpack = [&](int q) -> int {
     if (first[q] < 0) return ECW_OK;
-    if (hipEventSynchronize(P.ev_out[q]) != hipSuccess) return ECW_EDEVICE;
+    if (hipEventSynchronize(P.ev_out[q]) != hipSuccess) return drain(P, ECW_EDEVICE);
     const uint8_t* h = c->h_stage + q * slot;
     const int s0 = first[q];
     copy_blocks(static_cast<size_t>(count[q]) * np, len, [&](size_t a, size_t b) {
@@ -863,7 +871,7 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
   int b = 0;
   for (int s0 = 0; s0 < stripes; s0 += per, ++b) {
     const int q = b & 1, ns = std::min(per, stripes - s0);
-    if ((st = unpack(q))) return st;
+    if ((st = unpack(q))) return drain(P, st);
     uint8_t* h = c->h_stage + q * slot;
     uint8_t* d = c->d_stage + q * slot;
     copy_blocks(static_cast<size_t>(ns) * k, len, [&](size_t a, size_t e) {
@@ -871,16 +879,16 @@ int encode_stripes_packed(ecw_codec* c, HostPipe& P, int stripes, const uint8_t*
         std::memcpy(h + (x / k) * sb_bytes + (x % k) * cs, data[static_cast<size_t>(s0) * k + x], len);
     });
     if (hipMemcpy2DAsync(d, sb_bytes, h, sb_bytes, k * cs, ns, hipMemcpyHostToDevice, P.s_run) != hipSuccess)
-      return ECW_EDEVICE;
+      return drain(P, ECW_EDEVICE);
     const SlabRows slab = slab_rows(d, cs, sb_bytes, k);
     EncodeTarget t;
     t.slab = &slab;
     t.stripes = ns;
-    if ((st = run_encode(c, t, len, P.s_run))) return st;
+    if ((st = run_encode(c, t, len, P.s_run))) return drain(P, st);
     if (hipMemcpy2DAsync(h + k * cs, sb_bytes, d + k * cs, sb_bytes, np * cs, ns, hipMemcpyDeviceToHost,
                          P.s_run) != hipSuccess ||
         hipEventRecord(P.ev_out[q], P.s_run) != hipSuccess)
-      return ECW_EDEVICE;
+      return drain(P, ECW_EDEVICE);
     first[q] = s0;
     count[q] = ns;
   }
@@ -925,30 +933,30 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
       const int slot = static_cast<int>(step % kSlots);
       const size_t n = std::min(chunk, len - c0);
       uint8_t* base = c->d_stage + slot * slot_bytes;
-      if (step >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      if (step >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
       for (int s = 0; s < ns; ++s)
         for (int j = 0; j < k; ++j)
           if (hipMemcpyAsync(base + s * stripe_bytes + j * cstride, data[static_cast<size_t>(s0 + s) * k + j] + c0, n,
                              hipMemcpyHostToDevice, P.s_in) != hipSuccess)
-            return ECW_EDEVICE;
-      if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return ECW_EDEVICE;
-      if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return ECW_EDEVICE;
+            return drain(P, ECW_EDEVICE);
+      if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
+      if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
       const SlabRows slab = slab_rows(base, cstride, stripe_bytes, k);
       EncodeTarget t;
       t.slab = &slab;
       t.stripes = ns;
-      if ((st = run_encode(c, t, n, P.s_run))) return st;
-      if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return ECW_EDEVICE;
-      if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return ECW_EDEVICE;
+      if ((st = run_encode(c, t, n, P.s_run))) return drain(P, st);
+      if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return drain(P, ECW_EDEVICE);
+      if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
       for (int s = 0; s < ns; ++s)
         for (int i = 0; i < np; ++i)
           if (hipMemcpyAsync(parity[static_cast<size_t>(s0 + s) * np + i] + c0, base + s * stripe_bytes + (k + i) * cstride,
                              n, hipMemcpyDeviceToHost, P.s_out) != hipSuccess)
-            return ECW_EDEVICE;
-      if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return ECW_EDEVICE;
+            return drain(P, ECW_EDEVICE);
+      if (hipEventRecord(P.ev_out[slot], P.s_out) != hipSuccess) return drain(P, ECW_EDEVICE);
     }
   }
-  if (hipStreamSynchronize(P.s_out) != hipSuccess) return ECW_EDEVICE;
+  if (hipStreamSynchronize(P.s_out) != hipSuccess) return drain(P, ECW_EDEVICE);
   return hipStreamSynchronize(P.s_run) == hipSuccess ? ECW_OK : ECW_EDEVICE;
 }
 
