@@ -217,8 +217,8 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
         xs.base = t.slab->base;
         xs.bstride = t.slab->bstride;
         xs.sstride = t.slab->sstride;
-        xs.out = t.slab->pbase + static_cast<uint64_t>(m + i) * t.slab->bstride;
-        xs.ostride = t.slab->sstride;
+        xs.out = t.slab->pbase + static_cast<uint64_t>(m + i) * t.slab->pbstride;
+        xs.ostride = t.slab->psstride;
         for (int u = 0; u < n; ++u) xs.idx[u] = j0 + u;
         if (lmode == kLocalZero) {
           for (int st = 0; st < t.stripes; ++st)
@@ -597,6 +597,33 @@ int ecw_encode_batch_dev(ecw_codec* c, uint8_t* d_slab, size_t block_stride, siz
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
   const SlabRows slab = slab_rows(d_slab, block_stride, stripe_stride, c->k());
+  EncodeTarget t;
+  t.slab = &slab;
+  t.stripes = stripes;
+  return run_encode(c, t, len, static_cast<hipStream_t>(stream));
+}
+
+int ecw_encode_batch_split_dev(ecw_codec* c, const uint8_t* d_data, size_t data_block_stride,
+                               size_t data_stripe_stride, uint8_t* d_parity, size_t parity_block_stride,
+                               size_t parity_stripe_stride, int stripes, size_t len, void* stream) {
+  if (!c || !d_data || !d_parity || stripes < 0 || !check_len(len)) return ECW_EINVAL;
+  const size_t k = static_cast<size_t>(c->k()), np = static_cast<size_t>(c->info.parity_num);
+  if ((k > 1 && len > data_block_stride) || (np > 1 && len > parity_block_stride)) return ECW_EINVAL;
+  if (!aligned16(d_data) || !aligned16(d_parity) || data_block_stride % 16 || data_stripe_stride % 16 ||
+      parity_block_stride % 16 || parity_stripe_stride % 16)
+    return ECW_EALIGN;
+  if (stripes > 1 && (data_stripe_stride < (k - 1) * data_block_stride + len ||
+                      parity_stripe_stride < (np - 1) * parity_block_stride + len))
+    return ECW_EINVAL;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int st = c->ensure_device();
+    if (st) return st;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  const SlabRows slab{d_data, data_block_stride, data_stripe_stride, d_parity, parity_block_stride,
+                      parity_stripe_stride};
   EncodeTarget t;
   t.slab = &slab;
   t.stripes = stripes;

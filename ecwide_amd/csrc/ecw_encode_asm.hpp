@@ -193,7 +193,8 @@
   "29:\n\t"
 
 // Block pointers. SLAB: %[row0] / %[lrow0] / %[grow0] are the first data,
-// local and global blocks, all %[bslo]/%[bshi] apart. TAB (pointer mode):
+// local and global blocks; data blocks are %[bslo]/%[bshi] apart, parity
+// blocks %[pbslo]/%[pbshi]. TAB (pointer mode):
 // they are the addresses of pointer tables in the kernel arguments
 // (PtrRows::src, &dst[nrows], &dst[0]), and every block pointer is an
 // s_load. The row pointer for the next ring load is fetched right after the
@@ -208,13 +209,13 @@
 #define ECW_LPTR_INIT_TAB "s_mov_b32 s61, 0\n\t"
 #define ECW_LPTR_GET_SLAB
 #define ECW_LPTR_GET_TAB "s_load_dwordx2 s[42:43], %[lrow0], s61\n\ts_waitcnt lgkmcnt(0)\n\t"
-#define ECW_LPTR_NEXT_SLAB "s_add_u32 s42, s42, %[bslo]\n\ts_addc_u32 s43, s43, %[bshi]\n\t"
+#define ECW_LPTR_NEXT_SLAB "s_add_u32 s42, s42, %[pbslo]\n\ts_addc_u32 s43, s43, %[pbshi]\n\t"
 #define ECW_LPTR_NEXT_TAB "s_add_u32 s61, s61, 8\n\t"
 #define ECW_GPTR_INIT_SLAB "s_mov_b64 s[54:55], %[grow0]\n\t"
 #define ECW_GPTR_INIT_TAB "s_mov_b32 s62, 0\n\t"
 #define ECW_GPTR_GET_SLAB
 #define ECW_GPTR_GET_TAB "s_load_dwordx2 s[54:55], %[grow0], s62\n\ts_waitcnt lgkmcnt(0)\n\t"
-#define ECW_GPTR_NEXT_SLAB "s_add_u32 s54, s54, %[bslo]\n\ts_addc_u32 s55, s55, %[bshi]\n\t"
+#define ECW_GPTR_NEXT_SLAB "s_add_u32 s54, s54, %[pbslo]\n\ts_addc_u32 s55, s55, %[pbshi]\n\t"
 #define ECW_GPTR_NEXT_TAB "s_add_u32 s62, s62, 8\n\t"
 #define ECW_LRESET_0
 #define ECW_LRESET_1 "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t"
@@ -333,7 +334,8 @@
 
 #define ECW_TILE_OPERANDS                                                          \
   : : [row0] "s"(row0), [lrow0] "s"(lrow0), [grow0] "s"(grow0), [bslo] "s"(bslo), \
-    [bshi] "s"(bshi), [k] "s"(k), [r] "s"(r), [nrows] "s"(nrows), [lds] "s"(lds), \
+    [bshi] "s"(bshi), [pbslo] "s"(pbslo), [pbshi] "s"(pbshi), [k] "s"(k), [r] "s"(r),  \
+    [nrows] "s"(nrows), [lds] "s"(lds),                                            \
     [col] "v"(col)                                                                 \
   : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18",  \
     "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32",  \
@@ -594,8 +596,10 @@ namespace {
 // NW = 1: <= 4 global rows (u32 table entries); NW = 2: 5-8 rows (u64 entries)
 template <int LOCAL, bool PARK, bool TAB, int NW = 1>
 __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
-                                                int k, int r, int nrows, uint32_t lds, uint32_t col) {
+                                                uint64_t pbstride, int k, int r, int nrows, uint32_t lds,
+                                                uint32_t col) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
+  const uint32_t pbslo = static_cast<uint32_t>(pbstride), pbshi = static_cast<uint32_t>(pbstride >> 32);
   if constexpr (NW == 2) {
     if constexpr (TAB) {
       ECW2_TILE_CALL(TAB)

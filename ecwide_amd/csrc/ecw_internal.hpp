@@ -31,13 +31,16 @@ struct PtrRows {
 
 struct SlabRows {
   const uint8_t* base;   // data block 0 of stripe 0
-  uint64_t bstride;      // bytes between blocks of a stripe
-  uint64_t sstride;      // bytes between stripes
-  uint8_t* pbase;        // parity block 0 (G0, then L0.. follow at bstride) of stripe 0
+  uint64_t bstride;      // bytes between data blocks of a stripe
+  uint64_t sstride;      // bytes between stripes (data)
+  uint8_t* pbase;        // parity block 0 (G0, then G1.., L0..) of stripe 0
+  uint64_t pbstride;     // bytes between parity blocks of a stripe
+  uint64_t psstride;     // bytes between stripes (parities)
 };
 // the slab layout proper: parities follow the k data blocks
 inline SlabRows slab_rows(const uint8_t* base, uint64_t bstride, uint64_t sstride, int k) {
-  return SlabRows{base, bstride, sstride, const_cast<uint8_t*>(base) + static_cast<uint64_t>(k) * bstride};
+  return SlabRows{base, bstride, sstride, const_cast<uint8_t*>(base) + static_cast<uint64_t>(k) * bstride,
+                  bstride, sstride};
 }
 
 struct EncodeGeom {

@@ -142,13 +142,13 @@ __device__ __forceinline__ uint8_t* glob_row(const PtrRows& r, const EncodeGeom&
   return r.dst[l];
 }
 __device__ __forceinline__ uint8_t* glob_row(const SlabRows& r, const EncodeGeom& g, int s, int l) {
-  return r.pbase + s * r.sstride + static_cast<uint64_t>(g.row0 + l) * r.bstride;
+  return r.pbase + s * r.psstride + static_cast<uint64_t>(g.row0 + l) * r.pbstride;
 }
 __device__ __forceinline__ uint8_t* local_row(const PtrRows& r, const EncodeGeom& g, int, int t) {
   return r.dst[g.nrows + t];
 }
 __device__ __forceinline__ uint8_t* local_row(const SlabRows& r, const EncodeGeom& g, int s, int t) {
-  return r.pbase + s * r.sstride + static_cast<uint64_t>(g.m + t) * r.bstride;
+  return r.pbase + s * r.psstride + static_cast<uint64_t>(g.m + t) * r.pbstride;
 }
 
 // ---- GF(2^8) multiply-accumulate of one 16-byte row slice -----------------
@@ -374,20 +374,19 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
     const TileAt cur = tile_at(g, tile);
     if (cur.full) {
       if constexpr (std::is_same<Rows, SlabRows>::value) {
-        const uint64_t bs = rows.bstride;
-        const uint64_t so = static_cast<uint64_t>(cur.s) * rows.sstride;
-        const uint8_t* sb = uniform_ptr(rows.base + so);
-        const uint8_t* pb = uniform_ptr(rows.pbase + so);
-        encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * bs),
-                                            const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * bs), bs, k, r,
-                                            nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+        const uint64_t bs = rows.bstride, pbs = rows.pbstride;
+        const uint8_t* sb = uniform_ptr(rows.base + static_cast<uint64_t>(cur.s) * rows.sstride);
+        const uint8_t* pb = uniform_ptr(rows.pbase + static_cast<uint64_t>(cur.s) * rows.psstride);
+        encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * pbs),
+                                                const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * pbs), bs,
+                                                pbs, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
       } else {
         const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
             reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
         const uint8_t* dtab = ka + offsetof(PtrRows, dst);
         encode_tile_asm<LOCAL, PARK, true, NW>(ka + offsetof(PtrRows, src),
                                            const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
-                                           const_cast<uint8_t*>(dtab), 0, k, r, nrows,
+                                           const_cast<uint8_t*>(dtab), 0, 0, k, r, nrows,
                                            __builtin_amdgcn_readfirstlane(lds_base), cur.col);
       }
     } else {

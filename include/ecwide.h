@@ -218,6 +218,17 @@ int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* 
 /* Encode every stripe of the slab: reads D blocks, writes G and L blocks. */
 int ecw_encode_batch_dev(ecw_codec* codec, uint8_t* d_slab, size_t block_stride,
                          size_t stripe_stride, int stripes, size_t len, void* stream);
+/* The same encode with data and parity blocks in separate strided regions
+ * (ISA-L's separate data / coding arrays, isal:include/erasure_code.h:98, as
+ * strided batches): data block j of stripe s at
+ * d_data + s*data_stripe_stride + j*data_block_stride, parity block i
+ * ([G_0..G_{m-1}, L_0..L_{g-1}]) at d_parity + s*parity_stripe_stride +
+ * i*parity_block_stride. The regions must not overlap. With 4 KiB "stripes"
+ * (block stride 4096, stripe stride k*4096) it encodes a tiled layout in
+ * which every 4 KiB column of the k data blocks is contiguous. */
+int ecw_encode_batch_split_dev(ecw_codec* codec, const uint8_t* d_data, size_t data_block_stride,
+                               size_t data_stripe_stride, uint8_t* d_parity, size_t parity_block_stride,
+                               size_t parity_stripe_stride, int stripes, size_t len, void* stream);
 /* Repair block `lost_block` (slab block index, D or L; G is "not yet" in the
  * reference, ClMetadataManager.java:179-182) of every stripe into
  * d_out + s*out_stride, as the XOR of its surviving group members. */

@@ -145,6 +145,39 @@ def test_column_slices_match_full_encode(E, torch, orc):
             assert np.array_equal(pbuf[i, :B].cpu().numpy(), w), (world, i)
 
 
+@pytest.mark.parametrize("k,m,r,B,S,tiled", [(128, 3, 27, 4096, 6, True), (32, 6, 8, 4096, 3, True),
+                                              (20, 11, 6, 3 * 4096 + 48, 2, False), (9, 2, 3, 5000, 3, False)])
+def test_split_layout_encode_vs_oracle(E, torch, orc, k, m, r, B, S, tiled):
+    """ecw_encode_batch_split_dev: data and parities in separate regions. tiled:
+    4 KiB stripes with contiguous columns (block stride 4096, stripe stride
+    k*4096); otherwise padded strides; the padding past each block untouched."""
+    from ctypes import c_void_p
+
+    from ecwide_amd._lib import lib
+
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    np_ = c.parityNum
+    dbs = B if tiled else (B + 255) // 256 * 256 + 4096
+    pbs = B if tiled else (B + 255) // 256 * 256 + 512
+    dss, pss = k * dbs, np_ * pbs + (0 if tiled else 4096)
+    data = torch.empty(S * dss, dtype=torch.uint8, device="cuda")
+    par = torch.full((S * pss,), 0x5A, dtype=torch.uint8, device="cuda")
+    stream = c_void_p(torch.cuda.current_stream().cuda_stream)
+    assert lib.ecw_fill_random_dev(0, c_void_p(data.data_ptr()), dbs, dss, S, k, B, 31, 0, 0, stream) == 0
+    st = lib.ecw_encode_batch_split_dev(c._h, c_void_p(data.data_ptr()), dbs, dss, c_void_p(par.data_ptr()), pbs,
+                                        pss, S, B, stream)
+    assert st == 0
+    torch.cuda.synchronize()
+    oc = orc.codec("C", k, m, r, B)
+    pn = par.cpu().numpy()
+    for s in range(S):
+        want = oc.encode([orc.fill(B, 31, s, j) for j in range(k)], threads=8)
+        for i in range(np_):
+            o = s * pss + i * pbs
+            assert np.array_equal(pn[o:o + B], want[i]), (s, i)
+            assert (pn[o + B:o + pbs] == 0x5A).all(), ("wrote past the block", s, i)
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]

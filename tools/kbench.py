@@ -35,6 +35,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=0,
                     help="chunk-interleaved layout: each stripe stored as B/CHUNK column chunks, "
                          "the k+m+g blocks' chunks adjacent (timed as B/CHUNK mini-stripes)")
+    ap.add_argument("--split", action="store_true",
+                    help="with --chunk: data chunks in one region, parities in another "
+                         "(ecw_encode_batch_split_dev; encode only)")
     a = ap.parse_args()
     import torch
 
@@ -62,6 +65,12 @@ def main():
         assert L.ecw_codec_create(byref(sch), 1, 0, 1 if a.literal else 0, 0, byref(h)) == 0
         libs.append((os.path.basename(path), L, h))
     L0 = libs[0][1]
+    if a.split:
+        assert a.chunk and a.pad == 0, "--split needs --chunk and --pad 0"
+        del buf
+        buf = torch.empty(S * k * B, dtype=torch.uint8, device="cuda")
+        pbuf = torch.empty(S * (m + g) * B, dtype=torch.uint8, device="cuda")
+        bstride, sstride = B, k * B
     assert L0.ecw_fill_random_dev(0, c_void_p(buf.data_ptr()), bstride, sstride, S, k, B, 1, 0, 0, stream) == 0
     enc_bytes = S * nblk * B
     rep_bytes = S * (r + 1) * B
@@ -82,7 +91,11 @@ def main():
             for it in range(a.iters + 1):
                 if it == 1:
                     e[0].record()
-                if a.ptr:
+                if a.split:
+                    st = L.ecw_encode_batch_split_dev(h, c_void_p(buf.data_ptr()), B, k * B,
+                                                      c_void_p(pbuf.data_ptr()), B, (m + g) * B, S, B, stream)
+                    assert st == 0, (name, st)
+                elif a.ptr:
                     for s_ in range(S):
                         st = L.ecw_encode_dev(h, dptrs[s_], pptrs[s_], B, stream)
                         assert st == 0, (name, st)
@@ -90,7 +103,7 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            for it in range(a.iters if a.code == "C" and not a.literal else 0):  # literal L blocks cannot repair
+            for it in range(a.iters if a.code == "C" and not a.literal and not a.split else 0):  # literal L: no repair
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
                                             c_void_p(out.data_ptr()), B, B, stream)
                 assert st == 0, (name, st)
