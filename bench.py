@@ -29,6 +29,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--layout", choices=["blocks", "tiled"], default="blocks",
+                    help="slab layout in HBM (ecwide_amd/slab.py): whole blocks at a padded stride, or "
+                         "tiled (each --chunk-kib column piece of the k data blocks contiguous, parities apart)")
+    ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
@@ -241,7 +245,8 @@ def main():
         s0, S = stripe_shard(S_total, world, rank) if args.strong else weak_shard(S, rank)
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
     codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
-    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local)
+    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local, layout=args.layout,
+                        chunk=args.chunk_kib << 10)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
     slab.fill_random(seed=args.seed, s0=s0)
     torch.cuda.synchronize()
@@ -290,10 +295,20 @@ def main():
         import oracle
 
         orc = oracle.Oracle()
-        oc = orc.codec("C", k, m, r, B)
-        data = [orc.fill(B, args.seed, 0, j) for j in range(k)]
-        want = oc.encode(data, threads=min(os.cpu_count() or 1, 32))
-        ok = all(np.array_equal(p.cpu().numpy(), w) for p, w in zip(slab.parity(0), want))
+        if args.layout == "tiled":
+            # every (stripe, piece) unit is an independent stripe of `chunk` bytes
+            ch = slab.chunk
+            oc = orc.codec("C", k, m, r, ch)
+            par0 = [p.cpu().numpy() for p in slab.parity(0)]
+            ok = True
+            for piece in (0, slab.pieces - 1):
+                want = oc.encode([orc.fill(ch, args.seed, piece, j) for j in range(k)])
+                ok = ok and all(np.array_equal(p[piece * ch:(piece + 1) * ch], w) for p, w in zip(par0, want))
+        else:
+            oc = orc.codec("C", k, m, r, B)
+            data = [orc.fill(B, args.seed, 0, j) for j in range(k)]
+            want = oc.encode(data, threads=min(os.cpu_count() or 1, 32))
+            ok = all(np.array_equal(p.cpu().numpy(), w) for p, w in zip(slab.parity(0), want))
         ok = ok and torch.equal(out[:B], slab.block(0, 0))
 
     if rank != 0:
@@ -337,6 +352,9 @@ def main():
                                              f"{slab.buf.numel() / 2**30:.1f} GiB slab]" if args.hbm_fill else ""),
             "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B, "stripes_per_gpu": S, "stripes_total": S_total,
             "parallelism": f"stripe-partitioned x{world} (no collectives on the data path)",
+            "layout": ("blocks (each block contiguous, block stride B + 4 KiB)" if args.layout == "blocks" else
+                       f"tiled ({args.chunk_kib} KiB column pieces: the k data pieces contiguous, "
+                       f"parities in their own region)"),
             "encode_bytes_per_step_per_gpu": enc_bytes,
             "repair_bytes_per_step_per_gpu": rep_bytes,
         },

@@ -83,6 +83,8 @@ SIGNATURES = {
     "ecw_encode_batch_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_size_t, c_void_p]),
     "ecw_encode_batch_split_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, c_size_t,
                                            c_int, c_size_t, c_void_p]),
+    "ecw_repair_batch_split_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, c_size_t,
+                                           c_int, c_int, c_void_p, c_size_t, c_size_t, c_void_p]),
     "ecw_repair_batch_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_int, c_void_p, c_size_t,
                                      c_size_t, c_void_p]),
     "ecw_repair_sources": (c_int, [c_void_p, c_int, POINTER(c_int), c_int]),

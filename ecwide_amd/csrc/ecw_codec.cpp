@@ -214,12 +214,11 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
       if (t.slab) {
         XorSlab xs;
         std::memset(&xs, 0, sizeof xs);
-        xs.base = t.slab->base;
-        xs.bstride = t.slab->bstride;
-        xs.sstride = t.slab->sstride;
+        int idx[kMaxSrc];
+        for (int u = 0; u < n; ++u) idx[u] = j0 + u;
+        xor_sources(xs, *t.slab, k, idx, n);
         xs.out = t.slab->pbase + static_cast<uint64_t>(m + i) * t.slab->pbstride;
         xs.ostride = t.slab->psstride;
-        for (int u = 0; u < n; ++u) xs.idx[u] = j0 + u;
         if (lmode == kLocalZero) {
           for (int st = 0; st < t.stripes; ++st)
             if (hipMemsetAsync(xs.out + st * xs.ostride, 0, len, s) != hipSuccess) return ECW_EDEVICE;
@@ -650,27 +649,45 @@ int ecw_repair_sources(const ecw_codec* c, int lost, int* out, int cap) {
   return w;
 }
 
+static int repair_rows(ecw_codec* c, const SlabRows& rows, int stripes, int lost_block, uint8_t* d_out,
+                       size_t out_stride, size_t len, hipStream_t stream) {
+  if (c->info.local_mode == ECW_LOCAL_LITERAL) return ECW_EUNSUPPORTED;  // literal L blocks are zeros
+  int idx[kMaxSrc];
+  const int n = ecw_repair_sources(c, lost_block, idx, kMaxSrc);
+  if (n < 0) return n;
+  if (n == 0) return ECW_EUNSUPPORTED;
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  XorSlab xs;
+  std::memset(&xs, 0, sizeof xs);
+  xor_sources(xs, rows, c->k(), idx, n);
+  xs.out = d_out;
+  xs.ostride = out_stride;
+  XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
+  if (len == 0 || stripes == 0) return ECW_OK;
+  return status_of(launch_xor_slab(xs, xg, stream));
+}
+
 int ecw_repair_batch_dev(ecw_codec* c, const uint8_t* d_slab, size_t block_stride, size_t stripe_stride,
                          int stripes, int lost_block, uint8_t* d_out, size_t out_stride, size_t len, void* stream) {
   if (!c || !d_slab || !d_out || stripes < 0 || !check_len(len) || len > block_stride) return ECW_EINVAL;
   if (!aligned16(d_slab) || !aligned16(d_out) || block_stride % 16 || stripe_stride % 16 || out_stride % 16)
     return ECW_EALIGN;
-  if (c->info.local_mode == ECW_LOCAL_LITERAL) return ECW_EUNSUPPORTED;  // literal L blocks are zeros
-  XorSlab xs;
-  std::memset(&xs, 0, sizeof xs);
-  const int n = ecw_repair_sources(c, lost_block, xs.idx, kMaxSrc);
-  if (n < 0) return n;
-  if (n == 0) return ECW_EUNSUPPORTED;
-  DeviceGuard g(c->device);
-  if (!g.ok) return ECW_EDEVICE;
-  xs.base = d_slab;
-  xs.bstride = block_stride;
-  xs.sstride = stripe_stride;
-  xs.out = d_out;
-  xs.ostride = out_stride;
-  XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
-  if (len == 0 || stripes == 0) return ECW_OK;
-  return status_of(launch_xor_slab(xs, xg, static_cast<hipStream_t>(stream)));
+  return repair_rows(c, slab_rows(d_slab, block_stride, stripe_stride, c->k()), stripes, lost_block, d_out,
+                     out_stride, len, static_cast<hipStream_t>(stream));
+}
+
+int ecw_repair_batch_split_dev(ecw_codec* c, const uint8_t* d_data, size_t data_block_stride,
+                               size_t data_stripe_stride, const uint8_t* d_parity, size_t parity_block_stride,
+                               size_t parity_stripe_stride, int stripes, int lost_block, uint8_t* d_out,
+                               size_t out_stride, size_t len, void* stream) {
+  if (!c || !d_data || !d_parity || !d_out || stripes < 0 || !check_len(len)) return ECW_EINVAL;
+  if (!aligned16(d_data) || !aligned16(d_parity) || !aligned16(d_out) || data_block_stride % 16 ||
+      data_stripe_stride % 16 || parity_block_stride % 16 || parity_stripe_stride % 16 || out_stride % 16)
+    return ECW_EALIGN;
+  const SlabRows rows{d_data, data_block_stride, data_stripe_stride, const_cast<uint8_t*>(d_parity),
+                      parity_block_stride, parity_stripe_stride};
+  return repair_rows(c, rows, stripes, lost_block, d_out, out_stride, len, static_cast<hipStream_t>(stream));
 }
 
 int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride, int stripes,

@@ -66,12 +66,23 @@ struct XorPtr {
   uint8_t* dst;
 };
 struct XorSlab {
-  const uint8_t* base;
-  uint64_t bstride, sstride;
+  const uint8_t* src0[kMaxSrc];  // source i in stripe 0
+  uint64_t sstride, psstride;    // stripe strides of the data / parity region
   uint8_t* out;
   uint64_t ostride;
-  int idx[kMaxSrc];      // source block indices within a stripe
+  uint8_t in_parity[kMaxSrc];    // source i lives in the parity region
 };
+// XOR sources = slab blocks idx[0..n) (data blocks < k, parities >= k)
+inline void xor_sources(XorSlab& xs, const SlabRows& rows, int k, const int* idx, int n) {
+  for (int i = 0; i < n; ++i) {
+    const bool par = idx[i] >= k;
+    xs.src0[i] = par ? rows.pbase + static_cast<uint64_t>(idx[i] - k) * rows.pbstride
+                     : rows.base + static_cast<uint64_t>(idx[i]) * rows.bstride;
+    xs.in_parity[i] = par ? 1 : 0;
+  }
+  xs.sstride = rows.sstride;
+  xs.psstride = rows.psstride;
+}
 struct XorGeom {
   uint64_t len, tiles;
   int stripes, n;

@@ -400,7 +400,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
 // ---- XOR reduce: dst = src_0 ^ ... ^ src_{n-1} ----------------------------
 __device__ __forceinline__ const uint8_t* xsrc(const XorPtr& a, int, int i) { return a.src[i]; }
 __device__ __forceinline__ const uint8_t* xsrc(const XorSlab& a, int s, int i) {
-  return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
+  return a.src0[i] + static_cast<uint64_t>(s) * (a.in_parity[i] ? a.psstride : a.sstride);
 }
 __device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
 __device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }

@@ -235,6 +235,12 @@ int ecw_encode_batch_split_dev(ecw_codec* codec, const uint8_t* d_data, size_t d
 int ecw_repair_batch_dev(ecw_codec* codec, const uint8_t* d_slab, size_t block_stride,
                          size_t stripe_stride, int stripes, int lost_block, uint8_t* d_out,
                          size_t out_stride, size_t len, void* stream);
+/* The same repair on the split layout of ecw_encode_batch_split_dev
+ * (`lost_block` is still a stripe block index: D_j = j, L_t = k + m + t). */
+int ecw_repair_batch_split_dev(ecw_codec* codec, const uint8_t* d_data, size_t data_block_stride,
+                               size_t data_stripe_stride, const uint8_t* d_parity, size_t parity_block_stride,
+                               size_t parity_stripe_stride, int stripes, int lost_block, uint8_t* d_out,
+                               size_t out_stride, size_t len, void* stream);
 /* The slab block indices whose XOR rebuilds `lost_block` (a10: the r
  * surviving members of its local group). Writes up to `cap` indices into
  * `out_blocks`, returns the count (>0) or a negative ecw_status. */

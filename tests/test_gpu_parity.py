@@ -178,6 +178,34 @@ def test_split_layout_encode_vs_oracle(E, torch, orc, k, m, r, B, S, tiled):
             assert (pn[o + B:o + pbs] == 0x5A).all(), ("wrote past the block", s, i)
 
 
+@pytest.mark.parametrize("k,m,r,B,S,chunk", [(128, 3, 27, 1 << 16, 2, 8192), (32, 6, 8, 4 * 4096, 2, 4096),
+                                              (20, 2, 5, 3 * 8192, 3, 8192)])
+def test_tiled_slab_encode_repair(E, torch, orc, k, m, r, B, S, chunk):
+    """StripeSlab(layout="tiled"): every (stripe, piece) unit vs the oracle, and
+    the split-layout repair of every D and L block rebuilds it exactly."""
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled", chunk=chunk)
+    slab.fill_random(seed=71)
+    slab.encode()
+    torch.cuda.synchronize()
+    oc = orc.codec("C", k, m, r, chunk)
+    for s in range(S):
+        data = [slab.block(s, j).cpu().numpy() for j in range(k)]
+        par = [p.cpu().numpy() for p in slab.parity(s)]
+        for piece in range(slab.pieces):
+            sl = slice(piece * chunk, (piece + 1) * chunk)
+            assert np.array_equal(data[0][sl], orc.fill(chunk, 71, s * slab.pieces + piece, 0))
+            want = oc.encode([d[sl] for d in data])
+            for i, w in enumerate(want):
+                assert np.array_equal(par[i][sl], w), (s, piece, i)
+    out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
+    for lost in list(range(k)) + [k + m + t for t in range(c.groupNum)]:
+        slab.repair(lost, out)
+        torch.cuda.synchronize()
+        for s in range(S):
+            assert torch.equal(out[s * B:(s + 1) * B], slab.block(s, lost)), (lost, s)
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]
