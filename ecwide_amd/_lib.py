@@ -112,7 +112,9 @@ def _torch_runtime_first() -> None:
         pass
 
 
-def load(path: str = LIB_PATH) -> ctypes.CDLL:
+def load(path: str = LIB_PATH, strict: bool = True) -> ctypes.CDLL:
+    """Load a libecwide.so build; strict=False skips entry points an older
+    build (a tuning variant under build/) does not export."""
     _torch_runtime_first()
     if not os.path.exists(path):
         raise ImportError(
@@ -120,6 +122,8 @@ def load(path: str = LIB_PATH) -> ctypes.CDLL:
             "(the HIP extension is the only implementation)")
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
+        if not strict and not hasattr(lib, name):
+            continue
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args

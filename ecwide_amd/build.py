@@ -17,7 +17,7 @@ OUT = os.path.join(HERE, "libecwide.so")
 SHIM_SRC = os.path.join(HERE, "csrc", "ecw_isal_shim.cpp")
 SHIM_OUT = os.path.join(HERE, "libecw_isal.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wno-unused-function",
+FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wmissing-field-initializers", "-Wno-unused-function",
          "-I" + os.path.join(REPO, "include")]
 
 

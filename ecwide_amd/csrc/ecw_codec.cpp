@@ -154,18 +154,23 @@ struct EncodeTarget {
 };
 
 // Pointer-mode rows that are really a strided layout (data blocks at one
-// stride, parity blocks -- globals then locals -- at the same stride, e.g. two
-// [k, B] / [m+g, B] tensors): describe them as a one-stripe slab, so the
-// encode takes the slab kernel (asm tile) instead of the pointer kernel.
+// stride, parity blocks -- globals then locals -- at one stride of their own,
+// e.g. two [k, B] / [m+g, B] tensors): describe them as a one-stripe slab, so
+// the encode takes the slab kernel (asm tile) instead of the pointer kernel.
 bool as_slab(const uint8_t* const* src, int k, uint8_t* const* dst, int np, SlabRows* out) {
   auto at = [](const void* p) { return static_cast<uint64_t>(reinterpret_cast<uintptr_t>(p)); };
   if (k < 2 || np < 1 || at(src[1]) <= at(src[0])) return false;
   const uint64_t bs = at(src[1]) - at(src[0]);
   for (int j = 2; j < k; ++j)
     if (at(src[j]) != at(src[0]) + j * bs) return false;
-  for (int i = 1; i < np; ++i)
-    if (at(dst[i]) != at(dst[0]) + i * bs) return false;
-  *out = SlabRows{src[0], bs, 0, dst[0]};
+  uint64_t pbs = bs;
+  if (np > 1) {
+    if (at(dst[1]) <= at(dst[0])) return false;
+    pbs = at(dst[1]) - at(dst[0]);
+    for (int i = 2; i < np; ++i)
+      if (at(dst[i]) != at(dst[0]) + i * pbs) return false;
+  }
+  *out = SlabRows{src[0], bs, 0, dst[0], pbs, 0};
   return true;
 }
 
@@ -214,11 +219,12 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
       if (t.slab) {
         XorSlab xs;
         std::memset(&xs, 0, sizeof xs);
-        int idx[kMaxSrc];
-        for (int u = 0; u < n; ++u) idx[u] = j0 + u;
-        xor_sources(xs, *t.slab, k, idx, n);
+        xs.base = t.slab->base;
+        xs.bstride = t.slab->bstride;
+        xs.sstride = t.slab->sstride;
         xs.out = t.slab->pbase + static_cast<uint64_t>(m + i) * t.slab->pbstride;
         xs.ostride = t.slab->psstride;
+        for (int u = 0; u < n; ++u) xs.idx[u] = j0 + u;
         if (lmode == kLocalZero) {
           for (int st = 0; st < t.stripes; ++st)
             if (hipMemsetAsync(xs.out + st * xs.ostride, 0, len, s) != hipSuccess) return ECW_EDEVICE;
@@ -649,6 +655,8 @@ int ecw_repair_sources(const ecw_codec* c, int lost, int* out, int cap) {
   return w;
 }
 
+// lost_block's sources as XOR sources over `rows`; a standard slab (parities
+// right after the data blocks, same strides) runs as one region
 static int repair_rows(ecw_codec* c, const SlabRows& rows, int stripes, int lost_block, uint8_t* d_out,
                        size_t out_stride, size_t len, hipStream_t stream) {
   if (c->info.local_mode == ECW_LOCAL_LITERAL) return ECW_EUNSUPPORTED;  // literal L blocks are zeros
@@ -658,14 +666,42 @@ static int repair_rows(ecw_codec* c, const SlabRows& rows, int stripes, int lost
   if (n == 0) return ECW_EUNSUPPORTED;
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
-  XorSlab xs;
-  std::memset(&xs, 0, sizeof xs);
-  xor_sources(xs, rows, c->k(), idx, n);
-  xs.out = d_out;
-  xs.ostride = out_stride;
   XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
   if (len == 0 || stripes == 0) return ECW_OK;
-  return status_of(launch_xor_slab(xs, xg, stream));
+  const int k = c->k();
+  const bool one_region = rows.pbase == rows.base + static_cast<uint64_t>(k) * rows.bstride &&
+                          rows.pbstride == rows.bstride && rows.psstride == rows.sstride;
+  if (one_region) {
+    XorSlab xs;
+    std::memset(&xs, 0, sizeof xs);
+    xs.base = rows.base;
+    xs.bstride = rows.bstride;
+    xs.sstride = rows.sstride;
+    xs.out = d_out;
+    xs.ostride = out_stride;
+    for (int i = 0; i < n; ++i) xs.idx[i] = idx[i];
+    return status_of(launch_xor_slab(xs, xg, stream));
+  }
+  XorSplit xs;
+  std::memset(&xs, 0, sizeof xs);
+  xs.base = rows.base;
+  xs.bstride = rows.bstride;
+  xs.sstride = rows.sstride;
+  xs.pbase = rows.pbase;
+  xs.pbstride = rows.pbstride;
+  xs.psstride = rows.psstride;
+  xs.out = d_out;
+  xs.ostride = out_stride;
+  for (int i = 0; i < n; ++i) {
+    if (idx[i] < k) {
+      if (xs.ndata != i) return ECW_EINVAL;  // ecw_repair_sources lists the data blocks first
+      ++xs.ndata;
+      xs.idx[i] = idx[i];
+    } else {
+      xs.idx[i] = idx[i] - k;
+    }
+  }
+  return status_of(launch_xor_split(xs, xg, stream));
 }
 
 int ecw_repair_batch_dev(ecw_codec* c, const uint8_t* d_slab, size_t block_stride, size_t stripe_stride,

@@ -66,29 +66,31 @@ struct XorPtr {
   uint8_t* dst;
 };
 struct XorSlab {
-  const uint8_t* src0[kMaxSrc];  // source i in stripe 0
-  uint64_t sstride, psstride;    // stripe strides of the data / parity region
+  const uint8_t* base;           // block j of stripe s at base + s*sstride + j*bstride
+  uint64_t bstride, sstride;
   uint8_t* out;
   uint64_t ostride;
-  uint8_t in_parity[kMaxSrc];    // source i lives in the parity region
+  int idx[kMaxSrc];              // source block indices within a stripe
 };
-// XOR sources = slab blocks idx[0..n) (data blocks < k, parities >= k)
-inline void xor_sources(XorSlab& xs, const SlabRows& rows, int k, const int* idx, int n) {
-  for (int i = 0; i < n; ++i) {
-    const bool par = idx[i] >= k;
-    xs.src0[i] = par ? rows.pbase + static_cast<uint64_t>(idx[i] - k) * rows.pbstride
-                     : rows.base + static_cast<uint64_t>(idx[i]) * rows.bstride;
-    xs.in_parity[i] = par ? 1 : 0;
-  }
-  xs.sstride = rows.sstride;
-  xs.psstride = rows.psstride;
-}
+// Split layout (ecw_*_batch_split_dev): sources [0, ndata) are data blocks,
+// the rest parity blocks, each region with its own strides.
+struct XorSplit {
+  const uint8_t* base;
+  uint64_t bstride, sstride;
+  const uint8_t* pbase;
+  uint64_t pbstride, psstride;
+  uint8_t* out;
+  uint64_t ostride;
+  int ndata;
+  int idx[kMaxSrc];              // block index of source i within its region
+};
 struct XorGeom {
   uint64_t len, tiles;
   int stripes, n;
 };
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);
+hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s);
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes,
                               int nblocks, uint64_t len, uint64_t seed, int s0, int b0,

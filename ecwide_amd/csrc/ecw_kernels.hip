@@ -400,10 +400,15 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
 // ---- XOR reduce: dst = src_0 ^ ... ^ src_{n-1} ----------------------------
 __device__ __forceinline__ const uint8_t* xsrc(const XorPtr& a, int, int i) { return a.src[i]; }
 __device__ __forceinline__ const uint8_t* xsrc(const XorSlab& a, int s, int i) {
-  return a.src0[i] + static_cast<uint64_t>(s) * (a.in_parity[i] ? a.psstride : a.sstride);
+  return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
+}
+__device__ __forceinline__ const uint8_t* xsrc(const XorSplit& a, int s, int i) {
+  if (i < a.ndata) return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
+  return a.pbase + s * a.psstride + static_cast<uint64_t>(a.idx[i]) * a.pbstride;
 }
 __device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
 __device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }
+__device__ __forceinline__ uint8_t* xdst(const XorSplit& a, int s) { return a.out + s * a.ostride; }
 
 template <int P, bool TAIL, class Args>
 __device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s, uint32_t col) {
@@ -592,6 +597,7 @@ hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const v
 }
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
+hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes, int nblocks,
                               uint64_t len, uint64_t seed, int s0, int b0, hipStream_t s) {

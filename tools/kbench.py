@@ -58,7 +58,7 @@ def main():
     stream = c_void_p(torch.cuda.current_stream().cuda_stream)
     libs = []
     for path in a.libs:
-        L = _lib.load(path)
+        L = _lib.load(path, strict=False)
         sch = _lib.ecw_scheme()
         assert L.ecw_scheme_init(byref(sch), a.code.encode(), k, m, r, B) == 0
         h = c_void_p()
