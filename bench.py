@@ -238,7 +238,7 @@ def main():
         # fewer stripes than GPUs (SURVEY §8e fallback): every rank takes its
         # byte columns of every stripe instead
         s0 = 0
-        B = column_shard(B_full, world, rank)[1]
+        B = column_shard(B_full, world, rank, align=(args.chunk_kib << 10) if args.layout == "tiled" else 4096)[1]
         assert B > 0, "more GPUs than 4 KiB column tiles"
     else:
         # each rank owns distinct stripe ids; no data exchange between ranks
