@@ -29,10 +29,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--layout", choices=["blocks", "tiled"], default="blocks",
-                    help="slab layout in HBM (ecwide_amd/slab.py): whole blocks at a padded stride, or "
-                         "tiled (each --chunk-kib column piece of the k data blocks contiguous, parities apart)")
+    ap.add_argument("--layout", choices=["blocks", "tiled"], default="tiled",
+                    help="slab layout in HBM (ecwide_amd/slab.py): tiled (default; each --chunk-kib column piece "
+                         "of the k data blocks contiguous, parities apart) or whole blocks at a padded stride")
+    ap.add_argument("--other-layout-steps", type=int, default=5,
+                    help="N=1: also time this many steps on the other layout and report them in the line (0 = off)")
     ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
+    ap.add_argument("--unit-pad", type=int, default=0, help="tiled layout: padding after each piece run (bytes)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--k", type=int, default=128)
@@ -246,7 +249,7 @@ def main():
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
     codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local, layout=args.layout,
-                        chunk=args.chunk_kib << 10)
+                        chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
     slab.fill_random(seed=args.seed, s0=s0)
     torch.cuda.synchronize()
@@ -327,7 +330,7 @@ def main():
     if os.path.exists(args.pmc):
         try:
             pmc = json.load(open(args.pmc))
-            key = f"k{k}_r{r}_m{m}_B{B}_S{S}"
+            key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + (f"_tiled{args.chunk_kib}k" if args.layout == "tiled" else "")
             traffic = pmc.get(key, {}).get("encode_hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -378,6 +381,42 @@ def main():
     }
     if ok is not None:
         line["verified"] = bool(ok)
+    if world == 1 and args.other_layout_steps > 0 and not args.hbm_fill:
+        # the same workload on the other slab layout, for comparison (not `value`)
+        other = "blocks" if args.layout == "tiled" else "tiled"
+        del slab
+        torch.cuda.empty_cache()
+        slab2 = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local, layout=other,
+                             chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
+        slab2.fill_random(seed=args.seed, s0=s0)
+        n2 = args.other_layout_steps
+        for _ in range(2):
+            slab2.encode()
+            slab2.repair(0, out)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(n2):
+            slab2.encode()
+            slab2.repair(0, out)
+        torch.cuda.synchronize()
+        el2 = time.perf_counter() - t0
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        ev[0].record()
+        for _ in range(n2):
+            slab2.encode()
+        ev[1].record()
+        for _ in range(n2):
+            slab2.repair(0, out)
+        ev[2].record()
+        torch.cuda.synchronize()
+        line["other_layout"] = {
+            "layout": other, "steps": n2,
+            "value": round(step_bytes * n2 / el2 / 1e9, 2),
+            "encode_GBps": round(enc_bytes * n2 / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9, 2),
+            "repair_GBps": round(rep_bytes * n2 / (ev[1].elapsed_time(ev[2]) * 1e-3) / 1e9, 2),
+        }
+        del slab2
+        torch.cuda.empty_cache()
     if world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(args, k, m, r)
     print(json.dumps(line), flush=True)

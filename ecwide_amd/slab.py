@@ -30,7 +30,7 @@ DEFAULT_CHUNK = 8192
 class StripeSlab:
     def __init__(self, codec: NativeCodec, stripes: int, block_bytes: int | None = None,
                  pad: int = DEFAULT_PAD, device: int | None = None, layout: str = "blocks",
-                 chunk: int = DEFAULT_CHUNK):
+                 chunk: int = DEFAULT_CHUNK, unit_pad: int = 0):
         import torch
 
         self.codec = codec
@@ -48,19 +48,24 @@ class StripeSlab:
         elif layout == "tiled":
             if chunk % 256 or chunk <= 0 or self.len % chunk:
                 raise ValueError("tiled layout: chunk must be a positive multiple of 256 dividing the block size")
+            if unit_pad % 256:
+                raise ValueError("unit_pad must be a multiple of 256")
             self.chunk = chunk
             self.pieces = self.len // chunk           # column pieces per block
             self.units = stripes * self.pieces        # independent (stripe, piece) stripes
-            self.parity_offset = (self.units * k * chunk + 4095) // 4096 * 4096
-            nbytes = self.parity_offset + self.units * np_ * chunk
+            self.unit_stride = k * chunk + unit_pad   # data bytes per unit (+ padding)
+            self.punit_stride = np_ * chunk + unit_pad
+            self.parity_offset = (self.units * self.unit_stride + 4095) // 4096 * 4096
+            nbytes = self.parity_offset + self.units * self.punit_stride
         else:
             raise ValueError(f"unknown layout {layout!r}")
         self.buf = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
         self.base = self.buf.data_ptr()
 
     def _split_args(self):
-        k, np_, ch = self.codec.encodeDataNum, self.codec.parityNum, self.chunk
-        return (c_void_p(self.base), ch, k * ch, c_void_p(self.base + self.parity_offset), ch, np_ * ch)
+        ch = self.chunk
+        return (c_void_p(self.base), ch, self.unit_stride, c_void_p(self.base + self.parity_offset), ch,
+                self.punit_stride)
 
     # views ------------------------------------------------------------------
     def block(self, s: int, b: int):
@@ -70,9 +75,9 @@ class StripeSlab:
             return self.buf[o:o + self.len]
         k, np_, ch = self.codec.encodeDataNum, self.codec.parityNum, self.chunk
         if b < k:
-            o, step = s * self.pieces * k * ch + b * ch, k * ch
+            o, step = s * self.pieces * self.unit_stride + b * ch, self.unit_stride
         else:
-            o, step = self.parity_offset + s * self.pieces * np_ * ch + (b - k) * ch, np_ * ch
+            o, step = self.parity_offset + s * self.pieces * self.punit_stride + (b - k) * ch, self.punit_stride
         return self.buf.as_strided((self.pieces, ch), (step, 1), o).reshape(-1)
 
     def data(self, s: int):
@@ -88,7 +93,7 @@ class StripeSlab:
         (tiled layout: unit u = stripe * pieces + piece is PRNG stripe s0 * pieces + u)."""
         k = self.codec.encodeDataNum
         if self.layout == "tiled":
-            _check(lib.ecw_fill_random_dev(self.codec.device, c_void_p(self.base), self.chunk, k * self.chunk,
+            _check(lib.ecw_fill_random_dev(self.codec.device, c_void_p(self.base), self.chunk, self.unit_stride,
                                            self.units, k, self.chunk, seed, s0 * self.pieces, 0, _stream()),
                    "fill_random")
             return

@@ -11,7 +11,7 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 400 python bench.py --verify > gpurun_out/bench.log 2>&1 || exit $?
 tail -1 gpurun_out/bench.log
 cd /tmp
-P="python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --cpu-seconds 0"
+P="python3 $GRAFT_REPO_ROOT/bench.py --steps 5 --warmup 1 --cpu-seconds 0 --other-layout-steps 0"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/prof_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/prof.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_fetch_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc1.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/pmc_write_$TAG -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/pmc2.log 2>&1 || exit $?
