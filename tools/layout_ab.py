@@ -26,20 +26,25 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--variants", default="blocks:4096,tiled:8192:0,tiled:8192:4096,tiled:8192:256,tiled:4096:0")
+    ap.add_argument("--libs", default="", help="comma-separated libecwide.so builds to compare (default: the in-tree one)")
     a = ap.parse_args()
     import torch
 
     from ecwide_amd import _lib
 
-    L = _lib.lib
+    libs = [(os.path.basename(p), _lib.load(p, strict=False)) for p in a.libs.split(",") if p] or [("", _lib.lib)]
+    L = libs[0][1]
     k, m, r, S = a.k, a.m, a.r, a.stripes
     B = a.mib << 20
     g = -(-k // r)
     np_ = m + g
     sch = _lib.ecw_scheme()
     assert L.ecw_scheme_init(byref(sch), b"C", k, m, r, B) == 0
-    h = c_void_p()
-    assert L.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(h)) == 0
+    handles = []
+    for _, Lx in libs:
+        hx = c_void_p()
+        assert Lx.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(hx)) == 0
+        handles.append(hx)
     stream = c_void_p(torch.cuda.current_stream().cuda_stream)
     variants = []
     need = 0
@@ -62,9 +67,9 @@ def main():
     out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
     base = buf.data_ptr()
     enc_bytes, rep_bytes = S * (k + np_) * B, S * (r + 1) * B
-    res = {v[0]: ([], []) for v in variants}
+    res = {}
 
-    def run(v, what):
+    def run(v, what, L, h):
         name, kind, geo, _, _ = v
         if kind == "blocks":
             bs = geo
@@ -85,24 +90,27 @@ def main():
 
     for _ in range(a.rounds):
         for v in variants:
-            assert run(v, "fill") == 0
-            assert run(v, "enc") == 0 and run(v, "rep") == 0
-            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-            e[0].record()
-            for _ in range(a.iters):
-                assert run(v, "enc") == 0
-            e[1].record()
-            for _ in range(a.iters):
-                assert run(v, "rep") == 0
-            e[2].record()
-            torch.cuda.synchronize()
-            res[v[0]][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
-            res[v[0]][1].append(rep_bytes * a.iters / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9)
+            for (lname, Lx), hx in zip(libs, handles):
+                key = (v[0] + " " + lname).strip()
+                res.setdefault(key, ([], []))
+                assert run(v, "fill", Lx, hx) == 0
+                assert run(v, "enc", Lx, hx) == 0 and run(v, "rep", Lx, hx) == 0
+                e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+                e[0].record()
+                for _ in range(a.iters):
+                    assert run(v, "enc", Lx, hx) == 0
+                e[1].record()
+                for _ in range(a.iters):
+                    assert run(v, "rep", Lx, hx) == 0
+                e[2].record()
+                torch.cuda.synchronize()
+                res[key][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
+                res[key][1].append(rep_bytes * a.iters / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9)
     print(f"CL(k={k},r={r},m={m}) B={a.mib} MiB x{S} stripes, one allocation; GB/s median over {a.rounds} rounds")
     for name, (en, rp) in res.items():
         ee, rr = statistics.median(en), statistics.median(rp)
         step = (enc_bytes + rep_bytes) / (enc_bytes / ee + rep_bytes / rr)
-        print(f"{name:26s} encode {ee:8.1f}  repair {rr:8.1f}  step {step:8.1f}", flush=True)
+        print(f"{name:40s} encode {ee:8.1f}  repair {rr:8.1f}  step {step:8.1f}", flush=True)
 
 
 if __name__ == "__main__":
