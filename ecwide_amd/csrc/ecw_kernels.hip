@@ -444,6 +444,53 @@ __global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom
   }
 }
 
+// Source count known at compile time (n <= ECW_XOR_FIXED_MAX, every CL repair
+// of a group of up to that many blocks): straight-line code, no loop. The
+// runtime-n ring above compiles to a loop whose head waits vmcnt(0) (LLVM's
+// waitcnt pass merges the prologue's and the back-edge's load orders), i.e.
+// every wave drains its loads every P rows; straight-line code gets exact
+// counted waits, and the source indices come in as one scalar batch.
+// Loads are issued with at most W in flight per wave (W >= N: all at once).
+#ifndef ECW_XOR_WINDOW
+#define ECW_XOR_WINDOW 8
+#endif
+template <int N, bool TAIL, class Args>
+__device__ __forceinline__ void xor_tile_fixed(const Args& a, const XorGeom& g, int s, uint32_t col) {
+  const uint32_t len = static_cast<uint32_t>(g.len);
+  if (TAIL && col >= len) return;
+  constexpr int W = ECW_XOR_WINDOW > 0 && ECW_XOR_WINDOW < N ? ECW_XOR_WINDOW : N;
+  uint4 v[N];
+  uint4 acc = make_uint4(0, 0, 0, 0);
+  // the scheduling barriers pin the issue order (the machine scheduler would
+  // otherwise pull the first XORs up between the first loads: vmcnt(0) after two)
+#pragma unroll
+  for (int i = 0; i < N; ++i) {
+    v[i] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, i), col, len);
+    __builtin_amdgcn_sched_barrier(0);
+    if (i >= W - 1) {
+      acc = xor4(acc, v[i - W + 1]);
+      if (W < N) asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w));  // keep the XOR here
+    }
+  }
+#pragma unroll
+  for (int i = N - W + 1; i < N; ++i) acc = xor4(acc, v[i]);
+  st16<TAIL, ECW_XOR_NT>(xdst(a, s), col, len, acc);
+}
+
+template <int N, class Args>
+__global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g) {
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
+  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+    const int s = static_cast<int>(tile / g.tiles);
+    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+    const uint32_t col = col0 + threadIdx.x * kLaneBytes;
+    if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
+      xor_tile_fixed<N, false>(a, g, s, col);
+    else
+      xor_tile_fixed<N, true>(a, g, s, col);
+  }
+}
+
 // ---- synthetic fill (ecwide.h: ecw_fill_random_dev) ------------------------
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z ^= z >> 30;
@@ -490,6 +537,9 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
 #endif
 #ifndef ECW_GRID_PER_CU
 #define ECW_GRID_PER_CU 256  // encode: workgroups per CU before tiles are grid-strided (256 vs 64: +2.7 %)
+#endif
+#ifndef ECW_XOR_FIXED_MAX
+#define ECW_XOR_FIXED_MAX 32  // XOR reduce over n <= this many sources: straight-line kernel per n (0: off)
 #endif
 #ifndef ECW_GRID_PER_CU_XOR
 #define ECW_GRID_PER_CU_XOR 2048  // XOR reduce: one workgroup per tile up to 512 Ki tiles (+8.6 % at the HBM-filling batch vs 512)
@@ -568,6 +618,16 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
   return hipSuccess;
 }
 
+template <int N, class Args>
+hipError_t launch_xor_fixed(const Args& a, const XorGeom& g, dim3 grid, hipStream_t s) {
+  if constexpr (N >= 1) {
+    if (g.n < N) return launch_xor_fixed<N - 1>(a, g, grid, s);
+    hipLaunchKernelGGL((xor_kernel_fixed<N, Args>), grid, dim3(kBlock), 0, s, a, g);
+    return hipGetLastError();
+  }
+  return hipErrorInvalidValue;
+}
+
 template <class Args>
 hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
@@ -576,6 +636,7 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   // ring depth <= n: the ring refills past the last row re-read row n-1, so a
   // depth-8 ring over 1-2 sources would load every byte up to 8 times
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR)), block(kBlock);
+  if (g.n <= ECW_XOR_FIXED_MAX) return launch_xor_fixed<ECW_XOR_FIXED_MAX>(a, g, grid, s);
   if (g.n <= 1)
     hipLaunchKernelGGL((xor_kernel<1, Args>), grid, block, 0, s, a, g);
   else if (g.n <= 2)
