@@ -103,22 +103,24 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            for it in range(a.iters if a.code == "C" and not a.literal and not a.split else 0):  # literal L: no repair
+            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split else 0  # literal L: no repair
+            for it in range(rep_iters):
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
                                             c_void_p(out.data_ptr()), B, B, stream)
                 assert st == 0, (name, st)
             e[2].record()
             torch.cuda.synchronize()
             res[name][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
-            res[name][1].append(rep_bytes * a.iters / (max(e[1].elapsed_time(e[2]), 1e-6) * 1e-3) / 1e9)
+            if rep_iters:
+                res[name][1].append(rep_bytes * rep_iters / (max(e[1].elapsed_time(e[2]), 1e-6) * 1e-3) / 1e9)
             if ref is not None and "ablate" not in name:
                 got = buf[(k) * bstride:(k) * bstride + B]
                 if not torch.equal(got, ref):
                     print(f"  !! {name}: parity differs from {libs[0][0]}")
     print(f"{a.code}(k={k},r={r},m={m}) B={B} x{S} stripes pad={a.pad}; GB/s median (min..max) over {a.rounds} rounds")
     for name, (en, rp) in res.items():
-        print(f"{name:28s} encode {statistics.median(en):8.1f} ({min(en):7.1f}..{max(en):7.1f})   "
-              f"repair {statistics.median(rp):8.1f} ({min(rp):7.1f}..{max(rp):7.1f})", flush=True)
+        rep = f"repair {statistics.median(rp):8.1f} ({min(rp):7.1f}..{max(rp):7.1f})" if rp else "repair  (not run)"
+        print(f"{name:28s} encode {statistics.median(en):8.1f} ({min(en):7.1f}..{max(en):7.1f})   {rep}", flush=True)
 
 
 if __name__ == "__main__":
