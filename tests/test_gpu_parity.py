@@ -206,6 +206,41 @@ def test_tiled_slab_encode_repair(E, torch, orc, k, m, r, B, S, chunk):
             assert torch.equal(out[s * B:(s + 1) * B], slab.block(s, lost)), (lost, s)
 
 
+def test_xor_every_source_count(E, torch, orc):
+    """XOR reduce at every source count of the straight-line kernels (1..32)
+    and past it (the ring kernel: 33, 40, 64, 129), full and ragged tiles,
+    against the oracle's XOR (pointer mode)."""
+    for n in list(range(1, 34)) + [40, 64, 129]:
+        ln = 4096 * 2 + 16 * (n % 7) + (n % 3)  # ragged tail for most n
+        data = [orc.fill(ln, 300 + n, 0, j) for j in range(n)]
+        d = dev_blocks(torch, n, ln, data)
+        out = torch.full((ln,), 0xA5, dtype=torch.uint8, device="cuda")
+        E.xor_reduce(d, out)
+        torch.cuda.synchronize()
+        assert np.array_equal(out.cpu().numpy(), orc.xor_blocks(data)), n
+
+
+@pytest.mark.parametrize("layout", ["blocks", "tiled"])
+@pytest.mark.parametrize("k,r", [(40, 40), (64, 31), (64, 32), (70, 33), (12, 1)])
+def test_repair_group_sizes(E, torch, k, r, layout):
+    """CL repair of D0, the group's last block and L0 with r + 1 survivors on
+    both sides of the straight-line kernel limit (32 sources), block slab
+    and tiled slab."""
+    B = 3 * 8192
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, 2, r, B), 1, False)
+    kw = {"layout": "tiled", "chunk": 8192} if layout == "tiled" else {}
+    slab = E.StripeSlab(c, stripes=2, block_bytes=B, **kw)
+    slab.fill_random(seed=7 + r)
+    slab.encode()
+    o = B if layout == "tiled" else slab.out_stride
+    out = torch.empty(2 * o, dtype=torch.uint8, device="cuda")
+    for lost in (0, min(r, k) - 1, k + 2):
+        slab.repair(lost, out)
+        torch.cuda.synchronize()
+        for s in range(2):
+            assert torch.equal(out[s * o:s * o + B], slab.block(s, lost)), (lost, s)
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]
