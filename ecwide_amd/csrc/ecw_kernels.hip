@@ -205,6 +205,20 @@ __device__ __forceinline__ uint4 unpack_row(const uint32_t (&acc)[16 * NW], int 
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
+#ifndef ECW_XCD_REMAP
+#define ECW_XCD_REMAP 0  // 1: blocks b and b + 8 (one XCD) take neighbouring tiles (tuning)
+#endif
+// First tile of this workgroup's grid-stride walk. Blocks are dealt round-robin
+// over the 8 XCDs; with the remap each XCD walks its own contiguous 1/8 of
+// every grid-sized window (a permutation of [0, gridDim.x) when 8 divides it).
+__device__ __forceinline__ uint64_t wg_slot() {
+#if ECW_XCD_REMAP
+  const uint32_t G = gridDim.x, b = blockIdx.x;
+  if ((G & 7u) == 0) return static_cast<uint64_t>(b & 7u) * (G >> 3) + (b >> 3);
+#endif
+  return blockIdx.x;
+}
+
 // Column tile `tile` of the slab: stripe, this lane's column, whole tile in range?
 struct TileAt {
   int s;
@@ -370,7 +384,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
-  for (uint64_t tile = g.tile_begin + blockIdx.x; tile < g.tile_end; tile += gridDim.x) {
+  for (uint64_t tile = g.tile_begin + wg_slot(); tile < g.tile_end; tile += gridDim.x) {
     const TileAt cur = tile_at(g, tile);
     if (cur.full) {
       if constexpr (std::is_same<Rows, SlabRows>::value) {
@@ -433,7 +447,7 @@ __device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s,
 template <int P, class Args>
 __global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom g) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  for (uint64_t tile = wg_slot(); tile < total; tile += gridDim.x) {
     const int s = static_cast<int>(tile / g.tiles);
     const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
     const uint32_t col = col0 + threadIdx.x * kLaneBytes;
@@ -480,7 +494,7 @@ __device__ __forceinline__ void xor_tile_fixed(const Args& a, const XorGeom& g, 
 template <int N, class Args>
 __global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
-  for (uint64_t tile = blockIdx.x; tile < total; tile += gridDim.x) {
+  for (uint64_t tile = wg_slot(); tile < total; tile += gridDim.x) {
     const int s = static_cast<int>(tile / g.tiles);
     const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
     const uint32_t col = col0 + threadIdx.x * kLaneBytes;
