@@ -326,12 +326,14 @@ def main():
     total_bytes = step_bytes * B_full // B // S * S_total * args.steps
     value = total_bytes / el_max / 1e9
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+    launches = slab.encode_launches()  # one encode() = `launches` equal kernel launches
     traffic = None
     if os.path.exists(args.pmc):
         try:
             pmc = json.load(open(args.pmc))
             key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + (f"_tiled{args.chunk_kib}k" if args.layout == "tiled" else "")
-            traffic = pmc.get(key, {}).get("encode_hbm_bytes_per_launch")
+            ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
+            traffic = ratio * enc_bytes / launches if ratio else None  # PMC bytes of one launch
         except Exception:
             traffic = None
     g = codec.groupNum
@@ -372,8 +374,12 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
             # PMC-measured HBM bytes of one launch over this run's launch time
-            "traffic_GBps": round(traffic / (enc_ms * 1e-3) / 1e9, 2) if traffic else None,
-            "launch_ms": round(enc_ms, 4),
+            "traffic_GBps": round(traffic * launches / (enc_ms * 1e-3) / 1e9, 2) if traffic else None,
+            # per kernel launch (rocprof's unit); one encode() of the slab = `launches` launches
+            "launch_ms": round(enc_ms / launches, 4),
+            "algorithmic_bytes_per_launch": enc_bytes // launches,
+            "launches_per_encode": launches,
+            "encode_call_ms": round(enc_ms, 4),
             "repair_launch_ms": round(rep_ms, 4),
             "repair_frac": round(rep_bytes / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
         },

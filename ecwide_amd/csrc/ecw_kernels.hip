@@ -603,8 +603,15 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
   return hipGetLastError();
 }
 
+// The slab is encoded in launch windows of one grid's worth of tiles (256 CUs x
+// ECW_GRID_PER_CU), one tile per workgroup, instead of one grid-strided launch:
+// a grid-strided workgroup jumps a whole grid ahead when it finishes, spreading
+// the in-flight tiles over several distant regions. Same allocation, interleaved:
+// +3.5 % encode at the 272 GiB HBM-filling slab (8 windows), +0.3..1.5 % at the
+// bench shape (2 windows) (profiles/r01_encode_launch_window_ab.log).
+// ECW_COHORT_TILES > 0 sets another window, < 0 launches the slab at once.
 #ifndef ECW_COHORT_TILES
-#define ECW_COHORT_TILES 0  // > 0: launch the slab in windows of this many tiles (tuning)
+#define ECW_COHORT_TILES 0
 #endif
 
 template <class Rows>
@@ -613,7 +620,9 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
   if (total == 0) return hipSuccess;
   if (g0.nrows < 1 || g0.nrows > kMaxPassRows || g0.k < 1 || g0.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
   const uint4* tbl = static_cast<const uint4*>(d_tbl);
-  const uint64_t win = ECW_COHORT_TILES > 0 ? static_cast<uint64_t>(ECW_COHORT_TILES) : total;
+  const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
+                       : ECW_COHORT_TILES == 0 ? 256ull * ECW_GRID_PER_CU
+                                               : total;
   for (uint64_t t0 = 0; t0 < total; t0 += win) {
     EncodeGeom g = g0;
     g.tile_begin = t0;

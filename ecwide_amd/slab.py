@@ -27,6 +27,10 @@ DEFAULT_PAD = 4096
 DEFAULT_CHUNK = 8192
 
 
+# launch_encode (ecw_kernels.hip) windows: 256 CUs x ECW_GRID_PER_CU (256) tiles per launch
+ENCODE_LAUNCH_TILES = 256 * 256
+
+
 class StripeSlab:
     def __init__(self, codec: NativeCodec, stripes: int, block_bytes: int | None = None,
                  pad: int = DEFAULT_PAD, device: int | None = None, layout: str = "blocks",
@@ -129,6 +133,15 @@ class StripeSlab:
     def encode_bytes(self) -> int:
         """Algorithmic bytes of one encode of the slab: (k + m + g) * B per stripe."""
         return self.stripes * self.nblocks * self.len
+
+    def encode_launches(self) -> int:
+        """Kernel launches one encode() makes: ceil(m / 8) row passes, each in
+        windows of ENCODE_LAUNCH_TILES 4 KiB column tiles (ecw_kernels.hip
+        launch_encode). For per-launch timings next to rocprof's."""
+        units, ulen = (self.units, self.chunk) if self.layout == "tiled" else (self.stripes, self.len)
+        tiles = units * -(-ulen // 4096)
+        passes = max(1, -(-self.codec.scheme.globalParityNum // 8))
+        return passes * -(-tiles // ENCODE_LAUNCH_TILES)
 
     def repair_bytes(self, lost_block: int) -> int:
         """(survivors + 1) * B per stripe: r reads + 1 write for a data block."""
