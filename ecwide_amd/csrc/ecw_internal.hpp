@@ -53,6 +53,7 @@ struct EncodeGeom {
   int local_mode;        // LocalMode
   uint64_t tile_begin;   // this launch covers slab tiles [tile_begin, tile_end)
   uint64_t tile_end;     //   (tile = stripe * tiles + column tile)
+  unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter (zeroed)
 };
 
 // Launchers return hipSuccess or the launch error.

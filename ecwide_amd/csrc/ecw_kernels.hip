@@ -373,12 +373,14 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 #define ECW_ASM_MIN_WAVES_NW2 4  // 128 VGPRs: the 8-row tile uses 110
 #endif
 
-#ifndef ECW_TICKET
-#define ECW_TICKET 0  // tuning only: one launch, workgroups take tiles in order from a global ticket
-#endif
-#if ECW_TICKET
-__device__ unsigned long long ecw_ticket;  // single-stream experiment: not safe for concurrent calls
-#endif
+// Next tile of a ticket-ordered launch (EncodeGeom::ticket): lane 0 of the
+// workgroup takes a ticket, the slot after the LDS tables hands it to the rest.
+__device__ __forceinline__ uint64_t take_ticket(const EncodeGeom& g, unsigned long long* slot) {
+  __syncthreads();  // every wave has read the previous ticket
+  if (threadIdx.x == 0) *slot = g.tile_begin + atomicAdd(g.ticket, 1ull);
+  __syncthreads();
+  return *slot;
+}
 
 template <int LOCAL, bool PARK, class Rows, int NW = 1>
 __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_WAVES_NW2) void encode_kernel_asm(
@@ -391,19 +393,12 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
-#if ECW_TICKET
   // the ticket slot sits after the tables: a static __shared__ variable would
   // shift the table records off the 64*NW alignment the LDS addressing relies on
-  unsigned long long* s_tile = reinterpret_cast<unsigned long long*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
-  for (;;) {
-    __syncthreads();
-    if (threadIdx.x == 0) *s_tile = g.tile_begin + atomicAdd(&ecw_ticket, 1ull);
-    __syncthreads();
-    const uint64_t tile = *s_tile;
-    if (tile >= g.tile_end) break;
-#else
-  for (uint64_t tile = g.tile_begin + wg_slot(); tile < g.tile_end; tile += gridDim.x) {
-#endif
+  unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
+  const bool tickets = g.ticket != nullptr;
+  for (uint64_t tile = tickets ? take_ticket(g, slot) : g.tile_begin + wg_slot(); tile < g.tile_end;
+       tile = tickets ? take_ticket(g, slot) : tile + gridDim.x) {
     const TileAt cur = tile_at(g, tile);
     if (cur.full) {
       if constexpr (std::is_same<Rows, SlabRows>::value) {
@@ -605,7 +600,7 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
 
 template <class Rows, int NW>
 hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
-  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + (ECW_TICKET ? 16 : 0);
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + 16;  // + ticket slot
   switch (g.local_mode) {
     case kLocalXor:
       if (g.groups <= kMaxParkedLocals)
@@ -632,6 +627,14 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 #ifndef ECW_COHORT_TILES
 #define ECW_COHORT_TILES 0
 #endif
+// Slabs of at least ECW_TICKET_MIN_TILES tiles (4 windows: 1 GiB of column per
+// data row, e.g. the 272 GiB HBM-filling batch) run as ONE launch whose
+// workgroups take tiles in order from a ticket counter: +2.9 % encode over the
+// windows at 240 x 8 MiB stripes, but -1.4..-9 % on smaller slabs
+// (profiles/r01_encode_ticket_ab.log). 0 disables.
+#ifndef ECW_TICKET_MIN_TILES
+#define ECW_TICKET_MIN_TILES (4ull * 256 * ECW_GRID_PER_CU)
+#endif
 
 template <class Rows>
 hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s) {
@@ -642,22 +645,28 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
                        : ECW_COHORT_TILES == 0 ? 256ull * ECW_GRID_PER_CU
                                                : total;
-#if ECW_TICKET
-  if (ECW_ENC_ASM && g0.k >= 2) {
+  if (ECW_ENC_ASM && g0.k >= 2 && ECW_TICKET_MIN_TILES > 0 && total >= ECW_TICKET_MIN_TILES) {
+    // one ticket-ordered launch; the counter is stream-ordered memory of its own,
+    // so concurrent calls on other streams never share it
     void* tp = nullptr;
-    hipError_t e = hipGetSymbolAddress(&tp, HIP_SYMBOL(ecw_ticket));
-    if (e == hipSuccess) e = hipMemsetAsync(tp, 0, sizeof(unsigned long long), s);
+    hipError_t e = hipMallocAsync(&tp, sizeof(unsigned long long), s);
     if (e != hipSuccess) return e;
-    EncodeGeom g = g0;
-    g.tile_begin = 0;
-    g.tile_end = total;
-    const dim3 grid(grid_for(total));
-    return g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
-                        : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+    e = hipMemsetAsync(tp, 0, sizeof(unsigned long long), s);
+    if (e == hipSuccess) {
+      EncodeGeom g = g0;
+      g.tile_begin = 0;
+      g.tile_end = total;
+      g.ticket = static_cast<unsigned long long*>(tp);
+      const dim3 grid(grid_for(total));
+      e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+                       : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+    }
+    const hipError_t f = hipFreeAsync(tp, s);
+    return e != hipSuccess ? e : f;
   }
-#endif
   for (uint64_t t0 = 0; t0 < total; t0 += win) {
     EncodeGeom g = g0;
+    g.ticket = nullptr;
     g.tile_begin = t0;
     g.tile_end = t0 + win < total ? t0 + win : total;
     const dim3 grid(grid_for(g.tile_end - g.tile_begin));

@@ -29,6 +29,7 @@ DEFAULT_CHUNK = 8192
 
 # launch_encode (ecw_kernels.hip) windows: 256 CUs x ECW_GRID_PER_CU (256) tiles per launch
 ENCODE_LAUNCH_TILES = 256 * 256
+TICKET_MIN_TILES = 4 * ENCODE_LAUNCH_TILES  # ECW_TICKET_MIN_TILES: one ticket-ordered launch from here on
 
 
 class StripeSlab:
@@ -136,11 +137,14 @@ class StripeSlab:
 
     def encode_launches(self) -> int:
         """Kernel launches one encode() makes: ceil(m / 8) row passes, each in
-        windows of ENCODE_LAUNCH_TILES 4 KiB column tiles (ecw_kernels.hip
-        launch_encode). For per-launch timings next to rocprof's."""
+        windows of ENCODE_LAUNCH_TILES 4 KiB column tiles, or one ticket-ordered
+        launch from TICKET_MIN_TILES tiles on (ecw_kernels.hip launch_encode).
+        For per-launch timings next to rocprof's."""
         units, ulen = (self.units, self.chunk) if self.layout == "tiled" else (self.stripes, self.len)
         tiles = units * -(-ulen // 4096)
         passes = max(1, -(-self.codec.scheme.globalParityNum // 8))
+        if tiles >= TICKET_MIN_TILES and self.codec.encodeDataNum >= 2:
+            return passes  # one ticket-ordered launch per pass
         return passes * -(-tiles // ENCODE_LAUNCH_TILES)
 
     def repair_bytes(self, lost_block: int) -> int:
