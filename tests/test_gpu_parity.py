@@ -241,6 +241,31 @@ def test_repair_group_sizes(E, torch, k, r, layout):
             assert torch.equal(out[s * o:s * o + B], slab.block(s, lost)), (lost, s)
 
 
+def test_ticket_launch_matches_windows(E, torch, orc):
+    """A slab of >= 262,144 column tiles is encoded by one ticket-ordered
+    launch (ecw_kernels.hip launch_encode); each stripe encoded on its own
+    (65,536 tiles: the launch-window path) must give the same parities, and a
+    column sample must match the oracle."""
+    k, m, r, B, S = 4, 2, 2, 256 << 20, 4
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+    assert slab.encode_launches() == 1
+    slab.fill_random(seed=404)
+    slab.encode()
+    np_ = c.parityNum
+    pbuf = torch.empty((np_, B), dtype=torch.uint8, device="cuda")
+    oc = orc.codec("C", k, m, r, 8192)
+    for s in (0, S - 1):
+        c.encodeData([slab.block(s, j) for j in range(k)], [pbuf[i] for i in range(np_)])
+        torch.cuda.synchronize()
+        for i, p in enumerate(slab.parity(s)):
+            assert torch.equal(p, pbuf[i]), (s, i)
+        off = B - 8192  # last column tile: claimed last by the ticket order
+        want = oc.encode([slab.block(s, j)[off:].cpu().numpy() for j in range(k)])
+        for i, w in enumerate(want):
+            assert np.array_equal(pbuf[i][off:].cpu().numpy(), w), (s, i)
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]
