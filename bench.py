@@ -7,16 +7,29 @@ block D0 of every stripe from its r surviving group members (one launch).
 Algorithmic bytes per stripe: encode (k+m+g)*B, repair (r+1)*B (inputs +
 outputs, ISA-L's perf_print convention). GB = 1e9.
 
-Multi-GPU (launched by torch.distributed.run): each rank owns its own slab
-of `--stripes` stripes (distinct stripe ids), no data moves between GPUs;
-torch.distributed is used only for the barrier and the max-over-ranks time.
+Workloads (BASELINE.json configs):
+  * N=1 default — configs[2] shape: CL(k=128, r=27, m=3), 64 MiB blocks,
+    8 stripes (the metric's k=128 / 64 MiB point); stripe 0 is the stripe the
+    committed full-size digests pin (seed 103, tests/golden/manifest.json).
+  * N>1 default — configs[4]: the configs[3] batch (256 stripes, block size
+    sized so the whole batch fills ONE GPU's HBM) split by stripe over the N
+    ranks, same B at every N ("scaling": "strong"). `--weak` gives every rank
+    the N=1 slab instead; `--hbm-fill` runs configs[3] at N=1.
+
+Multi-GPU: `python bench.py --gpus N` starts N rank processes itself
+(torch.distributed.run in a child process, before any GPU call in this one)
+unless it already runs under torch.distributed.run. One process per GPU; each
+rank owns its stripes in its own HBM, no data moves between GPUs;
+torch.distributed (RCCL) only lines ranks up (barrier) and takes the max of
+the per-rank times.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
-import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -24,11 +37,14 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec, /opt/skills/guides/MI355X_MICROARCH.md
+HBM_FILL_STRIPES = 256  # BASELINE configs[3]
+DEFAULT_SEED = 103      # = manifest "cfg3_full": the bench's stripe 0 is the digest-pinned stripe
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=1,
+                    help="ranks (one per GPU); without a torch.distributed.run environment bench.py launches them")
     ap.add_argument("--layout", choices=["blocks", "tiled"], default="tiled",
                     help="slab layout in HBM (ecwide_amd/slab.py): tiled (default; each --chunk-kib column piece "
                          "of the k data blocks contiguous, parities apart) or whole blocks at a padded stride")
@@ -41,125 +57,277 @@ def parse():
     ap.add_argument("--k", type=int, default=128)
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--r", type=int, default=27)
-    ap.add_argument("--block-mib", type=float, default=64.0)
-    ap.add_argument("--stripes", type=int, default=8, help="stripes per GPU")
-    ap.add_argument("--seed", type=int, default=1)
+    ap.add_argument("--block-mib", type=float, default=None, help="block size (default 64; --hbm-fill: from free HBM)")
+    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (weak) or in total (strong); default 8")
+    ap.add_argument("--seed", type=int, default=DEFAULT_SEED)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline leg (0 = skip)")
-    ap.add_argument("--cpu-sample-mib", type=float, default=4.0)
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
-    ap.add_argument("--verify", action="store_true", help="check one stripe against the oracle after timing")
+    ap.add_argument("--no-verify", dest="verify", action="store_false",
+                    help="skip the parity check after timing (default: every rank checks sampled column pieces "
+                         "of its first/middle/last stripe against the oracle and every stripe's D0 repair; at the "
+                         "default shape stripe 0 is also checked against the committed full-size digests)")
+    ap.add_argument("--verify", dest="verify", action="store_true")
     ap.add_argument("--hbm-fill", action="store_true",
-                    help="BASELINE configs[3]: 256 stripes per GPU, block size = the largest whole MiB "
-                         "that fits the GPU's free HBM")
+                    help="BASELINE configs[3]: 256 stripes, block size = the largest whole MiB at which the "
+                         "batch fits one GPU's free HBM (the N>1 default, split over the ranks)")
     ap.add_argument("--strong", action="store_true",
-                    help="strong scaling (BASELINE configs[4]): --stripes (or the --hbm-fill batch) is the "
-                         "TOTAL, split by stripe across the ranks")
+                    help="strong scaling: --stripes (or the --hbm-fill batch) is the TOTAL, split by stripe")
+    ap.add_argument("--weak", action="store_true",
+                    help="N>1: every rank runs the N=1 slab (weak scaling) instead of the configs[4] split")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="no GPU: plan every rank's share and run the rank orchestration and timing reduction "
+                         "only (CPU test of the N>1 path; --dry-run-free-gib stands in for free HBM)")
+    ap.add_argument("--dry-run-free-gib", type=float, default=287.0)
     ap.add_argument("--pageable", action="store_true",
                     help="with --host-resident: ordinary pageable host blocks instead of pinned ones")
     ap.add_argument("--host-resident", action="store_true",
                     help="measure the PCIe-inclusive rate (pinned host blocks) instead")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def dist_setup(args):
-    import torch
+# ---- rank orchestration ------------------------------------------------------
+def free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
 
-    from ecwide_amd.shard import dist_env
 
-    world, rank, local = dist_env()
-    # one process per GPU; on a box with fewer GPUs than ranks (a rehearsal of
-    # the N>1 path) ranks share devices and the timing collective runs on gloo
-    ndev = max(1, torch.cuda.device_count())
-    dev = local % ndev
-    torch.cuda.set_device(dev)
-    if world > 1:
+def spawn_ranks(n: int, argv: list) -> int:
+    """Start n ranks of this script under torch.distributed.run in a child
+    process (never exec: this process has not touched the GPU and stays the
+    parent) and return its exit code; rank 0 prints the JSON line."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={free_port()}", os.path.abspath(__file__)] + argv
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
+
+
+class Dist:
+    """World/rank/device of this process and the few collectives the bench
+    uses (barrier, max, gather of one float per rank)."""
+
+    def __init__(self, args):
+        from ecwide_amd.shard import dist_env
+
+        self.world, self.rank, self.local = dist_env()
+        if self.world != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={self.world}")
+        self.dry = args.dry_run
+        self.dev, self.ndev, self.backend = None, 0, None
+        if not self.dry:
+            import torch
+
+            self.ndev = torch.cuda.device_count()
+            if self.ndev < 1:
+                raise SystemExit("bench.py: no GPU visible (use --dry-run for the CPU rehearsal)")
+            # one process per GPU; on a box with fewer GPUs than ranks (a
+            # rehearsal of the N>1 path) ranks share devices over gloo
+            self.dev = self.local % self.ndev
+            torch.cuda.set_device(self.dev)
+        self.distinct = self.dry or self.ndev >= self.world
+        if self.world > 1:
+            import torch
+            import torch.distributed as dist
+
+            if not self.distinct:
+                print(f"bench.py: rehearsal: {self.world} ranks share {self.ndev} GPU(s)", file=sys.stderr)
+            if self.dry or not self.distinct:
+                dist.init_process_group("gloo")
+            else:
+                dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.dev}"))
+            self.backend = dist.get_backend()
+
+    def _tensor(self, vals):
+        import torch
+
+        on_gpu = self.backend == "nccl"
+        return torch.tensor(vals, dtype=torch.float64, device=f"cuda:{self.dev}" if on_gpu else "cpu")
+
+    def barrier(self):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.barrier()
+
+    def reduce(self, x: float, op: str) -> float:
+        if self.world == 1:
+            return x
         import torch.distributed as dist
 
-        if ndev >= world:
-            dist.init_process_group("nccl", device_id=torch.device(f"cuda:{dev}"))
-        else:
-            dist.init_process_group("gloo")
-    return world, rank, dev
+        t = self._tensor([x])
+        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
+        return float(t.item())
 
-
-def barrier(world):
-    if world > 1:
+    def gather(self, x: float) -> list:
+        """x of every rank, in rank order (an all-reduce of a one-hot vector)."""
+        if self.world == 1:
+            return [x]
         import torch.distributed as dist
 
-        dist.barrier()
+        v = [0.0] * self.world
+        v[self.rank] = x
+        t = self._tensor(v)
+        dist.all_reduce(t)
+        return [float(a) for a in t.tolist()]
+
+    def close(self):
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.destroy_process_group()
 
 
-def max_over_ranks(world, x: float) -> float:
-    if world == 1:
-        return x
-    import torch
-    import torch.distributed as dist
+def plan(args, d: Dist, free_bytes: int, parity_num: int) -> dict:
+    """The workload and this rank's share of it (same on every rank except
+    the share). free_bytes: this GPU's free HBM before any allocation."""
+    from ecwide_amd.shard import hbm_fill_block_mib, plan_rank
 
-    on_gpu = dist.get_backend() == "nccl"
-    t = torch.tensor([x], dtype=torch.float64, device="cuda" if on_gpu else "cpu")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    k = args.k
+    fill = args.hbm_fill or (d.world > 1 and not args.weak and args.stripes is None and args.block_mib is None)
+    strong = args.strong or (fill and d.world > 1 and not args.weak)
+    if fill:
+        total = HBM_FILL_STRIPES
+        # the whole batch fits ONE GPU at this B, so B is the same at every N
+        # (ranks sharing a device in a rehearsal hold the batch between them)
+        mib = hbm_fill_block_mib(free_bytes, k, parity_num, total)
+        mib = int(d.reduce(float(mib), "min"))
+        if mib < 1:
+            raise SystemExit(f"bench.py: {free_bytes} B free: too small for {total} stripes")
+        block_mib = float(mib)
+    else:
+        total = args.stripes if args.stripes is not None else 8
+        block_mib = args.block_mib if args.block_mib is not None else 64.0
+    B = int(block_mib * (1 << 20))
+    align = (args.chunk_kib << 10) if args.layout == "tiled" else 4096
+    share = plan_rank(total, B, d.world, d.rank, strong, per_rank=total, align=align)
+    if share["block_bytes"] <= 0:
+        raise SystemExit("bench.py: more ranks than column tiles")
+    stripes_total = total if strong else total * d.world
+    return dict(hbm_fill=fill, strong=strong, stripes_total=stripes_total, block_bytes_full=B, share=share)
 
 
-def cpu_baseline(args, k, m, r):
+# ---- CPU baseline (oracle: test infrastructure, never the measured product) --
+def host_cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or platform.machine()
+
+
+def cpu_baseline(args, k, m, r, B):
     """The reference's CPU path restated (oracle, test infrastructure): ECWide-C
     encodeData = ec_encode_data with the AVX2 4-bit-split dot products
     (global rows) + one pass per local group, then decodeData of D0 (XOR of
-    the r survivors), timed on a bounded column sample of the same stripe."""
+    the r survivors), on ONE whole stripe of the bench workload (k blocks of
+    B bytes), single thread (ECWide-C's one ComputeWorker) and the box's
+    per-GPU share of cores."""
     import ctypes
 
     import numpy as np
 
     import oracle
+    from ecwide_amd.shard import host_threads
 
     orc = oracle.Oracle()
-    B = int(args.cpu_sample_mib * (1 << 20))
     oc = orc.codec("C", k, m, r, B)
-    data = [orc.fill(B, args.seed, 0, j) for j in range(k)]
+    rng = np.random.default_rng(args.seed)
+    data = [np.frombuffer(rng.bytes(B), np.uint8) for _ in range(k)]
     par = [np.zeros(B, np.uint8) for _ in range(oc.parity_num)]
     u8p = ctypes.POINTER(ctypes.c_uint8)
     dp = (u8p * k)(*[d.ctypes.data_as(u8p) for d in data])
     pp = (u8p * len(par))(*[p.ctypes.data_as(u8p) for p in par])
-    g = oc.group_num
-    per_stripe = (k + m + g + r + 1) * B
-
+    per_stripe = (k + oc.parity_num + r + 1) * B
     ones = orc.init_tables(r, 1, np.ones(r, np.uint8))
+    rep = np.zeros(B, np.uint8)
+    rp = (u8p * 1)(rep.ctypes.data_as(u8p))
+    srcs = data[1:r] + [par[m]]
+    sp = (u8p * r)(*[s.ctypes.data_as(u8p) for s in srcs])
 
     def run(threads):
         oc.encode_into(dp, pp, B, literal=False, threads=threads)
         # decodeData: ec_encode_data with the all-ones table (NativeCodec.cc:248)
-        return orc.encode_data(ones, data[1:r] + [par[m]], 1, avx2=True)[0]
+        orc.L.orc_encode_data_avx2(B, r, 1, ones.ctypes.data_as(u8p), sp, rp)
 
-    from ecwide_amd.shard import host_threads
-
-    t1 = host_threads()
     res = {}
-    for threads in sorted({1, t1}):
-        run(threads)  # warm
+    allc = host_threads()
+    for threads in sorted({1, allc}):
         n, t0 = 0, time.perf_counter()
         while True:
-            rep = run(threads)
+            run(threads)
             n += 1
             el = time.perf_counter() - t0
             if el > args.cpu_seconds / 2 or n >= 50:
                 break
-        assert np.array_equal(rep, data[0])
+        assert np.array_equal(rep, data[0]), "CPU baseline repair mismatch"
         res[threads] = n * per_stripe / el / 1e9
     return {
         "value": round(res[1], 3),
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"1 stripe CL(k={k},r={r},m={m}) column sample B={B >> 20} MiB: ECWide-C encodeData flow "
-                   f"(AVX2 nibble-pshufb dot products, global + per-group passes) + XOR repair of D0; "
-                   f"single thread = ECWide-C's one ComputeWorker thread"),
-        "value_all_cores": round(res[t1], 3),
-        "cores_all": t1,
-        "host_cpu": platform.processor() or platform.machine(),
+        "sample": (f"1 whole stripe of the workload, CL(k={k},r={r},m={m}) B={B >> 20} MiB: ECWide-C encodeData "
+                   f"flow (AVX2 nibble-pshufb port of ISA-L's gf_Nvect_dot_prod_avx2, global + per-group passes) "
+                   f"+ decodeData of D0; 1 thread = ECWide-C's one ComputeWorker thread"),
+        "value_all_cores": round(res[allc], 3),
+        "cores_all": allc,
+        "host_cpu": host_cpu_model(),
         "avx2": orc.have_avx2(),
     }
 
 
+# ---- verification (outside the timed region) ---------------------------------
+def verify(args, slab, out, pl, k, m, r) -> dict:
+    """Sampled parity vs the oracle (8 KiB column windows at the first,
+    middle and last piece of this rank's first/middle/last stripe; columns
+    are independent, so a window is an exact check of those bytes), every
+    stripe's D0 repair == D0 on the device, and at the default shape stripe 0
+    vs the committed full-size SHA-256 digests of manifest 'cfg3_full'."""
+    import hashlib
+
+    import numpy as np
+    import torch
+
+    import oracle
+
+    orc = oracle.Oracle()
+    sh = pl["share"]
+    B, S, s0, off0 = sh["block_bytes"], sh["stripes"], sh["s0"], sh["col_offset"]
+    res = {"windows": 0, "repairs": 0, "digests": False}
+    W = min(8192, B)
+    oc = orc.codec("C", k, m, r, W)
+    for s in sorted({0, S // 2, S - 1}):
+        par = slab.parity(s)
+        for off in sorted({0, (B // 2) // W * W, B - W}):
+            want = oc.encode([orc.fill(W, args.seed, s0 + s, j, off0 + off) for j in range(k)])
+            for i, w in enumerate(want):
+                if not np.array_equal(par[i][off:off + W].cpu().numpy(), w):
+                    return dict(res, ok=False, failed=f"stripe {s0 + s} parity {i} at column {off0 + off}")
+            res["windows"] += 1
+    for s in range(S):
+        if not torch.equal(out[s * B:(s + 1) * B], slab.block(s, 0)):
+            return dict(res, ok=False, failed=f"stripe {s0 + s} D0 repair")
+        res["repairs"] += 1
+    mf = os.path.join(REPO, "tests", "golden", "manifest.json")
+    if s0 == 0 and off0 == 0 and os.path.exists(mf):
+        e = next((x for x in json.load(open(mf)).get("full", []) if x["name"] == "cfg3_full"), None)
+        if e and (e["k"], e["m"], e["r"], e["len"], e["seed"]) == (k, m, r, B, args.seed):
+            got = [hashlib.sha256(p.cpu().numpy().tobytes()).hexdigest() for p in slab.parity(0)]
+            rep = hashlib.sha256(out[:B].cpu().numpy().tobytes()).hexdigest()
+            if got != e["parity_sha256"] or rep != e["repair_d0_sha256"]:
+                return dict(res, ok=False, failed="stripe 0 vs manifest cfg3_full digests")
+            res["digests"] = True
+    return dict(res, ok=True)
+
+
+# ---- the PCIe-inclusive rate --------------------------------------------------
 def host_resident(args):
     """PCIe-inclusive rate: blocks live in pinned host memory; ecw_encode /
     ecw_repair pipeline them through HBM with hipMemcpyAsync in and out.
@@ -171,7 +339,7 @@ def host_resident(args):
 
     torch.cuda.set_device(0)
     k, m, r = args.k, args.m, args.r
-    B = int(args.block_mib * (1 << 20))
+    B = int((args.block_mib or 64.0) * (1 << 20))
     codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
     nblk = k + codec.parityNum
     hb = torch.empty(nblk * B, dtype=torch.uint8, pin_memory=not args.pageable)
@@ -211,47 +379,60 @@ def host_resident(args):
     print(json.dumps(line), flush=True)
 
 
-def main():
-    args = parse()
-    import torch
+# ---- the bench ------------------------------------------------------------------
+def dry_run(args, d: Dist):
+    """The N>1 orchestration without a GPU: plans, a stand-in timed region
+    (each rank sleeps a rank-dependent time) and the same reductions."""
+    g = -(-args.k // args.r)
+    pl = plan(args, d, int(args.dry_run_free_gib * (1 << 30)), args.m + g)
+    d.barrier()
+    t0 = time.perf_counter()
+    time.sleep(0.05 * (1 + d.rank))
+    d.barrier()
+    el = time.perf_counter() - t0
+    el_max = d.reduce(el, "max")
+    shares = [d.gather(float(pl["share"][key])) for key in ("s0", "stripes", "block_bytes", "col_offset")]
+    per_rank = d.gather(el)
+    if d.rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": d.world, "scaling": "strong" if pl["strong"] else "weak",
+                          "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
+                          "block_bytes": pl["block_bytes_full"], "el_max": el_max, "rank_seconds": per_rank,
+                          "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
+                                     for a, b, c, o in zip(*shares)]}), flush=True)
+    d.close()
 
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # decide before anything touches the GPU; the ranks are fresh processes
+        sys.exit(spawn_ranks(args.gpus, argv))
     if args.host_resident:
         host_resident(args)
         return
-    world, rank, local = dist_setup(args)
+    d = Dist(args)
+    if args.dry_run:
+        dry_run(args, d)
+        return
+    import torch
+
     import ecwide_amd as E
 
     k, m, r = args.k, args.m, args.r
-    S = args.stripes
-    if args.hbm_fill:
-        S = 256
-        free = torch.cuda.mem_get_info(local)[0]
-        g0 = -(-k // r)
-        # slab: S * (k+m+g) blocks of B + 4 KiB pad, plus the S-block repair output
-        per_mib = S * ((k + m + g0) * ((1 << 20) + 4096) + (1 << 20))
-        args.block_mib = float(int(0.97 * free) // per_mib)
-        assert args.block_mib >= 1, f"{free} B free: too small for {S} stripes"
-    B = int(args.block_mib * (1 << 20))
-    from ecwide_amd.shard import column_shard, stripe_shard, weak_shard
-
-    S_total = S if args.strong else S * world
-    B_full = B
-    columns = args.strong and S_total < world
-    if columns:
-        # fewer stripes than GPUs (SURVEY §8e fallback): every rank takes its
-        # byte columns of every stripe instead
-        s0 = 0
-        B = column_shard(B_full, world, rank, align=(args.chunk_kib << 10) if args.layout == "tiled" else 4096)[1]
-        assert B > 0, "more GPUs than 4 KiB column tiles"
-    else:
-        # each rank owns distinct stripe ids; no data exchange between ranks
-        s0, S = stripe_shard(S_total, world, rank) if args.strong else weak_shard(S, rank)
+    g0 = -(-k // r)
+    pl = plan(args, d, torch.cuda.mem_get_info(d.dev)[0], m + g0)
+    sh = pl["share"]
+    B, S, s0 = sh["block_bytes"], sh["stripes"], sh["s0"]
+    B_full, S_total, columns = pl["block_bytes_full"], pl["stripes_total"], sh["columns"]
     scheme = E.CodingScheme.getClScheme(k, m, r, B)
-    codec = E.NativeCodec.getClCodec(scheme, 1, False, device=local)
-    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local, layout=args.layout,
+    codec = E.NativeCodec.getClCodec(scheme, 1, False, device=d.dev)
+    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=args.layout,
                         chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
-    out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{local}")
-    slab.fill_random(seed=args.seed, s0=s0)
+    out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{d.dev}")
+    slab.fill_random(seed=args.seed, s0=s0, col_offset=sh["col_offset"])
     torch.cuda.synchronize()
     enc_bytes = slab.encode_bytes()
     rep_bytes = slab.repair_bytes(0)
@@ -272,18 +453,20 @@ def main():
     torch.cuda.synchronize()
 
     # timed region: exactly K steps
-    barrier(world)
+    d.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     torch.cuda.synchronize()
-    barrier(world)
+    d.barrier()
     el = time.perf_counter() - t0
-    el_max = max_over_ranks(world, el)
+    el_max = d.reduce(el, "max")
+    rank_s = d.gather(el)
 
-    # per-kernel durations with events on the launch stream (separate pass,
-    # same work, so the timed region carries no event overhead)
+    # per-kernel durations with events on the launch stream (torch's current
+    # stream: slab.encode/repair launch on it) in a separate pass of the same
+    # work, so the timed region carries no event overhead
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
     for i in range(args.steps):
         step(evs[i])
@@ -291,34 +474,12 @@ def main():
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
     rep_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
 
-    ok = None
-    if args.verify and rank == 0 and not columns:
-        import numpy as np
-
-        import oracle
-
-        orc = oracle.Oracle()
-        if args.layout == "tiled":
-            # every (stripe, piece) unit is an independent stripe of `chunk` bytes
-            ch = slab.chunk
-            oc = orc.codec("C", k, m, r, ch)
-            par0 = [p.cpu().numpy() for p in slab.parity(0)]
-            ok = True
-            for piece in (0, slab.pieces - 1):
-                want = oc.encode([orc.fill(ch, args.seed, piece, j) for j in range(k)])
-                ok = ok and all(np.array_equal(p[piece * ch:(piece + 1) * ch], w) for p, w in zip(par0, want))
-        else:
-            oc = orc.codec("C", k, m, r, B)
-            data = [orc.fill(B, args.seed, 0, j) for j in range(k)]
-            want = oc.encode(data, threads=min(os.cpu_count() or 1, 32))
-            ok = all(np.array_equal(p.cpu().numpy(), w) for p, w in zip(slab.parity(0), want))
-        ok = ok and torch.equal(out[:B], slab.block(0, 0))
-
-    if rank != 0:
-        if world > 1:
-            import torch.distributed as dist
-
-            dist.destroy_process_group()
+    vres = None
+    if args.verify:
+        vres = verify(args, slab, out, pl, k, m, r)
+        ok_all = d.reduce(1.0 if vres["ok"] else 0.0, "min") > 0.5
+    if d.rank != 0:
+        d.close()
         return
 
     # every stripe costs the same bytes; in column mode each stripe's bytes are
@@ -337,32 +498,44 @@ def main():
         except Exception:
             traffic = None
     g = codec.groupNum
+    if pl["hbm_fill"]:
+        wl = (f"configs[{4 if d.world > 1 else 3}]: {S_total} independent CL(k={k}, r={r}, m={m}, g={g}) stripes "
+              f"of B={B_full >> 20} MiB blocks (the batch that fills one GPU's HBM, "
+              f"{S_total * (k + m + g) * B_full / 2**30:.0f} GiB)"
+              + (f", split by stripe over {d.world} GPUs: {S} on rank 0" if d.world > 1 else "")
+              + ": batched encode + repair of D0")
+    else:
+        wl = (f"CL(k={k}, r={r}, m={m}, g={g}) B={B_full >> 20} MiB, "
+              + (f"{S_total} stripes in total" if pl["strong"] else f"{S} stripes/GPU")
+              + ": batched encode + repair of D0")
+    if columns:
+        wl += f" [column-sliced: {B} of {B_full} B per block on rank 0]"
     line = {
         "metric": "device-resident encode + single-block-repair GB/s, wide stripe (shards in HBM)",
         "value": round(value, 2),
         "unit": "GB/s",
-        "n_gpus": world,
+        "n_gpus": d.world,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(el_max / args.steps * 1e3, 4),
         "higher_is_better": True,
-        "scaling": "strong" if args.strong else "weak",
+        "scaling": "strong" if pl["strong"] else "weak",
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic (counter PRNG, uniform random bytes, generated in HBM)",
+        "data": "synthetic (counter PRNG of include/ecwide.h, uniform random bytes, generated in HBM)",
         "config": {
-            "workload": (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S} stripes/GPU: batched encode + "
-                         f"repair of D0") + (f" [strong: {S_total} stripes in total]" if args.strong else "")
-            + (f" [column-sliced: {B} of {B_full} B per block on this rank]" if columns else "") + (" [configs[3]: 256 stripes filling HBM, "
-                                             f"{slab.buf.numel() / 2**30:.1f} GiB slab]" if args.hbm_fill else ""),
-            "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B, "stripes_per_gpu": S, "stripes_total": S_total,
-            "parallelism": f"stripe-partitioned x{world} (no collectives on the data path)",
+            "workload": wl,
+            "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B,
+            "stripes_per_gpu": S, "stripes_total": S_total, "seed": args.seed,
+            "parallelism": f"stripe-partitioned x{d.world} (no collectives on the data path)",
             "layout": ("blocks (each block contiguous, block stride B + 4 KiB)" if args.layout == "blocks" else
                        f"tiled ({args.chunk_kib} KiB column pieces: the k data pieces contiguous, "
                        f"parities in their own region)"),
             "encode_bytes_per_step_per_gpu": enc_bytes,
             "repair_bytes_per_step_per_gpu": rep_bytes,
         },
+        "rank_ms_per_step": [round(x / args.steps * 1e3, 4) for x in rank_s],
+        "devices_distinct": d.distinct,
         "encode_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 2),
         "repair_GBps": round(rep_bytes / (rep_ms * 1e-3) / 1e9, 2),
         "roofline": {
@@ -385,25 +558,29 @@ def main():
         },
         "cpu_baseline": None,
     }
-    if ok is not None:
-        line["verified"] = bool(ok)
-    if world == 1 and args.other_layout_steps > 0 and not args.hbm_fill:
+    if vres is not None:
+        line["verified"] = bool(ok_all)
+        line["verify"] = {key: vres[key] for key in ("windows", "repairs", "digests")} | (
+            {"failed": vres["failed"]} if not vres["ok"] else {})
+    if d.world == 1 and args.other_layout_steps > 0 and not pl["hbm_fill"]:
         # the same workload on the other slab layout, for comparison (not `value`)
         other = "blocks" if args.layout == "tiled" else "tiled"
         del slab
         torch.cuda.empty_cache()
-        slab2 = E.StripeSlab(codec, stripes=S, block_bytes=B, device=local, layout=other,
+        slab2 = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=other,
                              chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
         slab2.fill_random(seed=args.seed, s0=s0)
         n2 = args.other_layout_steps
+        out2 = out if out.numel() >= S * slab2.out_stride else torch.empty(S * slab2.out_stride, dtype=torch.uint8,
+                                                                           device=f"cuda:{d.dev}")
         for _ in range(2):
             slab2.encode()
-            slab2.repair(0, out)
+            slab2.repair(0, out2)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(n2):
             slab2.encode()
-            slab2.repair(0, out)
+            slab2.repair(0, out2)
         torch.cuda.synchronize()
         el2 = time.perf_counter() - t0
         ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
@@ -412,7 +589,7 @@ def main():
             slab2.encode()
         ev[1].record()
         for _ in range(n2):
-            slab2.repair(0, out)
+            slab2.repair(0, out2)
         ev[2].record()
         torch.cuda.synchronize()
         line["other_layout"] = {
@@ -423,13 +600,10 @@ def main():
         }
         del slab2
         torch.cuda.empty_cache()
-    if world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(args, k, m, r)
+    if d.world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)
     print(json.dumps(line), flush=True)
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.destroy_process_group()
+    d.close()
 
 
 if __name__ == "__main__":

@@ -73,9 +73,15 @@ struct ecw_codec {
   uint8_t* h_stage = nullptr;         // pinned host staging of the small-block path
   size_t h_stage_bytes = 0;
 
+  // ticket counters of big encodes, one per stream (ecw_internal.hpp
+  // TicketCounter); ticket_mu serialises the launches that use them
+  std::mutex ticket_mu;
+  std::map<hipStream_t, TicketCounter> tickets;
+
   ~ecw_codec() {
-    if (dev_ready || !d_pass.empty()) {
+    if (dev_ready || !d_pass.empty() || !tickets.empty()) {
       DeviceGuard g(device);
+      for (auto& kv : tickets) (void)hipFree(kv.second.ptr);
       for (void* p : d_pass) (void)hipFree(p);
       if (d_stage) (void)hipFree(d_stage);
       if (h_stage) (void)hipHostFree(h_stage);
@@ -111,6 +117,27 @@ struct ecw_codec {
     if (hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) return fail(ECW_EDEVICE);
     dev_ready = true;
     return ECW_OK;
+  }
+
+  // the counter of stream s (caller holds ticket_mu); null when it cannot be
+  // allocated: the encode then runs in launch windows
+  TicketCounter* ticket_for(hipStream_t s) {
+    auto it = tickets.find(s);
+    if (it != tickets.end()) return &it->second;
+    void* p = nullptr;
+    if (hipMalloc(&p, sizeof(unsigned long long)) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    if (hipMemsetAsync(p, 0, sizeof(unsigned long long), s) != hipSuccess) {
+      (void)hipGetLastError();
+      (void)hipFree(p);
+      return nullptr;
+    }
+    TicketCounter& t = tickets[s];
+    t.ptr = static_cast<unsigned long long*>(p);
+    t.next = 0;
+    return &t;
   }
 
   int ensure_stage(size_t bytes) {
@@ -198,7 +225,12 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
     g.local_mode = (q == 0 && locals_inline) ? lmode : kLocalNone;
     hipError_t e;
     if (t.slab) {
-      e = launch_encode_slab(*t.slab, g, c->d_pass[q], s);
+      if (encode_uses_ticket(g.tiles * static_cast<uint64_t>(t.stripes), k)) {
+        std::lock_guard<std::mutex> lk(c->ticket_mu);
+        e = launch_encode_slab(*t.slab, g, c->d_pass[q], s, c->ticket_for(s));
+      } else {
+        e = launch_encode_slab(*t.slab, g, c->d_pass[q], s, nullptr);
+      }
     } else {
       PtrRows rows;
       std::memset(&rows, 0, sizeof rows);
@@ -206,7 +238,12 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
       for (int l = 0; l < g.nrows; ++l) rows.dst[l] = t.dst[g.row0 + l];
       if (g.local_mode != kLocalNone)
         for (int i = 0; i < ng; ++i) rows.dst[g.nrows + i] = t.dst[m + i];
-      e = launch_encode_ptr(rows, g, c->d_pass[q], s);
+      if (encode_uses_ticket(g.tiles, k)) {
+        std::lock_guard<std::mutex> lk(c->ticket_mu);
+        e = launch_encode_ptr(rows, g, c->d_pass[q], s, c->ticket_for(s));
+      } else {
+        e = launch_encode_ptr(rows, g, c->d_pass[q], s, nullptr);
+      }
     }
     if (e != hipSuccess) return ECW_EDEVICE;
   }
@@ -733,8 +770,22 @@ int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t 
   if (!aligned16(d_dst) || block_stride % 16 || stripe_stride % 16) return ECW_EALIGN;
   DeviceGuard g(device);
   if (!g.ok) return ECW_EDEVICE;
-  return status_of(launch_fill_random(d_dst, block_stride, stripe_stride, stripes, nblocks, len, seed, s0, b0,
-                                      static_cast<hipStream_t>(stream)));
+  return status_of(launch_fill_random(d_dst, block_stride, stripe_stride, stripes, nblocks, len, len ? len : 1, 0,
+                                      0, seed, s0, b0, static_cast<hipStream_t>(stream)));
+}
+
+int ecw_fill_random_pieces_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride, int stripes,
+                               int nblocks, size_t len, size_t piece, size_t piece_stride, size_t offset,
+                               uint64_t seed, int s0, int b0, void* stream) {
+  if (!d_dst || stripes < 0 || nblocks < 0 || s0 < 0 || b0 < 0 || piece == 0) return ECW_EINVAL;
+  if (!aligned16(d_dst) || block_stride % 16 || stripe_stride % 16 || piece % 16 || piece_stride % 16 ||
+      offset % 16)
+    return ECW_EALIGN;
+  if (len > piece && piece_stride < piece) return ECW_EINVAL;
+  DeviceGuard g(device);
+  if (!g.ok) return ECW_EDEVICE;
+  return status_of(launch_fill_random(d_dst, block_stride, stripe_stride, stripes, nblocks, len, piece,
+                                      piece_stride, offset, seed, s0, b0, static_cast<hipStream_t>(stream)));
 }
 
 // ---- host-memory entry points (blocking) ------------------------------------

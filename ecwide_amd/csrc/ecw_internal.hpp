@@ -53,14 +53,30 @@ struct EncodeGeom {
   int local_mode;        // LocalMode
   uint64_t tile_begin;   // this launch covers slab tiles [tile_begin, tile_end)
   uint64_t tile_end;     //   (tile = stripe * tiles + column tile)
-  unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter (zeroed)
+  unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter
+  uint64_t ticket_base;        //   whose value at this launch's start is ticket_base
 };
 
-// Launchers return hipSuccess or the launch error.
+// Device counter of ticket-ordered encode launches, one per (codec, stream).
+// It is never reset: a launch whose grid has G workgroups over T tiles takes
+// exactly T + G tickets (every workgroup draws one past the end to stop), so
+// the host knows the counter's value at the start of the next launch on the
+// same stream. The owner serialises launches that use one counter.
+struct TicketCounter {
+  unsigned long long* ptr = nullptr;
+  uint64_t next = 0;
+};
+
+// Launchers return hipSuccess or the launch error (an earlier, unrelated HIP
+// error of the calling thread is cleared first, not reported). The encode
+// launchers run a slab of >= ECW_TICKET_MIN_TILES tiles as one ticket-ordered
+// launch when `tc` is given, else in launch windows.
 hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl,
-                             hipStream_t s);
+                             hipStream_t s, TicketCounter* tc);
 hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl,
-                              hipStream_t s);
+                              hipStream_t s, TicketCounter* tc);
+// true when an encode of `tiles` column tiles at k data rows would use a ticket counter
+bool encode_uses_ticket(uint64_t tiles, int k);
 
 struct XorPtr {
   const uint8_t* src[kMaxSrc];
@@ -94,8 +110,8 @@ hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s);
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes,
-                              int nblocks, uint64_t len, uint64_t seed, int s0, int b0,
-                              hipStream_t s);
+                              int nblocks, uint64_t len, uint64_t piece, uint64_t pstride,
+                              uint64_t offset, uint64_t seed, int s0, int b0, hipStream_t s);
 
 int device_cu_count(int device);
 

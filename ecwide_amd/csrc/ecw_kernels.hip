@@ -377,7 +377,7 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 // workgroup takes a ticket, the slot after the LDS tables hands it to the rest.
 __device__ __forceinline__ uint64_t take_ticket(const EncodeGeom& g, unsigned long long* slot) {
   __syncthreads();  // every wave has read the previous ticket
-  if (threadIdx.x == 0) *slot = g.tile_begin + atomicAdd(g.ticket, 1ull);
+  if (threadIdx.x == 0) *slot = g.tile_begin + (atomicAdd(g.ticket, 1ull) - g.ticket_base);
   __syncthreads();
   return *slot;
 }
@@ -529,12 +529,18 @@ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   return z;
 }
 
+// Byte i of a block is byte (offset + i) of its generator stream; it lands at
+// p + (i / piece) * pstride + i % piece (piece = len: one contiguous block; a
+// tiled slab scatters the block's column pieces, so both layouts hold the same
+// bytes). piece and offset are multiples of 16, so a 16-byte group never
+// straddles a piece.
 __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bstride, uint64_t sstride,
-                                                      int stripes, int nblocks, uint64_t len,
-                                                      uint64_t seed, int s0, int b0) {
+                                                      int stripes, int nblocks, uint64_t len, uint64_t piece,
+                                                      uint64_t pstride, uint64_t offset, uint64_t seed, int s0,
+                                                      int b0) {
   constexpr uint64_t G = 0x9E3779B97F4A7C15ull;
-  const uint64_t nw = (len + 7) / 8;
-  const uint64_t npair = (nw + 1) / 2;
+  const uint64_t npair = (len + 15) / 16;
+  const uint64_t wbase = offset / 8;
   for (int y = blockIdx.y; y < stripes * nblocks; y += gridDim.y) {
     const int s = y / nblocks, b = y - s * nblocks;
     const uint64_t key = mix64(seed + G * (1ull + static_cast<uint64_t>(s0 + s) * 65536ull +
@@ -542,15 +548,17 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
     uint8_t* p = dst + s * sstride + static_cast<uint64_t>(b) * bstride;
     for (uint64_t q = blockIdx.x * static_cast<uint64_t>(kBlock) + threadIdx.x; q < npair;
          q += static_cast<uint64_t>(gridDim.x) * kBlock) {
-      const uint64_t w0 = 2 * q;
+      const uint64_t w0 = wbase + 2 * q;
       const uint64_t v0 = mix64(key + w0 * G), v1 = mix64(key + (w0 + 1) * G);
-      const uint64_t off = 8 * w0;
-      if (off + 16 <= len) {
-        *reinterpret_cast<uint4*>(p + off) = make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(v0 >> 32),
-                                                        static_cast<uint32_t>(v1), static_cast<uint32_t>(v1 >> 32));
+      const uint64_t i0 = 16 * q;
+      const uint64_t pc = i0 / piece;
+      uint8_t* o = p + pc * pstride + (i0 - pc * piece);
+      if (i0 + 16 <= len) {
+        *reinterpret_cast<uint4*>(o) = make_uint4(static_cast<uint32_t>(v0), static_cast<uint32_t>(v0 >> 32),
+                                                  static_cast<uint32_t>(v1), static_cast<uint32_t>(v1 >> 32));
       } else {
-        for (int i = 0; i < 16 && off + i < len; ++i)
-          p[off + i] = static_cast<uint8_t>((i < 8 ? v0 >> (8 * i) : v1 >> (8 * (i - 8))));
+        for (int i = 0; i < 16 && i0 + i < len; ++i)
+          o[i] = static_cast<uint8_t>((i < 8 ? v0 >> (8 * i) : v1 >> (8 * (i - 8))));
       }
     }
   }
@@ -637,32 +645,27 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 #endif
 
 template <class Rows>
-hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s) {
+hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s, TicketCounter* tc) {
   const uint64_t total = static_cast<uint64_t>(g0.stripes) * g0.tiles;
   if (total == 0) return hipSuccess;
   if (g0.nrows < 1 || g0.nrows > kMaxPassRows || g0.k < 1 || g0.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  (void)hipGetLastError();  // report this call's launch errors, not an earlier one
   const uint4* tbl = static_cast<const uint4*>(d_tbl);
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
                        : ECW_COHORT_TILES == 0 ? 256ull * ECW_GRID_PER_CU
                                                : total;
-  if (ECW_ENC_ASM && g0.k >= 2 && ECW_TICKET_MIN_TILES > 0 && total >= ECW_TICKET_MIN_TILES) {
-    // one ticket-ordered launch; the counter is stream-ordered memory of its own,
-    // so concurrent calls on other streams never share it
-    void* tp = nullptr;
-    hipError_t e = hipMallocAsync(&tp, sizeof(unsigned long long), s);
-    if (e != hipSuccess) return e;
-    e = hipMemsetAsync(tp, 0, sizeof(unsigned long long), s);
-    if (e == hipSuccess) {
-      EncodeGeom g = g0;
-      g.tile_begin = 0;
-      g.tile_end = total;
-      g.ticket = static_cast<unsigned long long*>(tp);
-      const dim3 grid(grid_for(total));
-      e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
-                       : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
-    }
-    const hipError_t f = hipFreeAsync(tp, s);
-    return e != hipSuccess ? e : f;
+  if (tc && tc->ptr && encode_uses_ticket(total, g0.k)) {
+    // one ticket-ordered launch; the caller holds the counter for this stream
+    EncodeGeom g = g0;
+    g.tile_begin = 0;
+    g.tile_end = total;
+    g.ticket = tc->ptr;
+    g.ticket_base = tc->next;
+    const dim3 grid(grid_for(total));
+    const hipError_t e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+                                      : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+    if (e == hipSuccess) tc->next += total + grid.x;  // every workgroup draws one ticket past the end
+    return e;
   }
   for (uint64_t t0 = 0; t0 < total; t0 += win) {
     EncodeGeom g = g0;
@@ -698,6 +701,7 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
   if (total == 0) return hipSuccess;
   if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
+  (void)hipGetLastError();  // report this call's launch error, not an earlier one
   // ring depth <= n: the ring refills past the last row re-read row n-1, so a
   // depth-8 ring over 1-2 sources would load every byte up to 8 times
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR)), block(kBlock);
@@ -715,26 +719,34 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
 
 }  // namespace
 
-hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s) {
-  return launch_encode(rows, g, d_tbl, s);
+hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
+                             TicketCounter* tc) {
+  return launch_encode(rows, g, d_tbl, s, tc);
 }
-hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl, hipStream_t s) {
-  return launch_encode(slab, g, d_tbl, s);
+hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
+                              TicketCounter* tc) {
+  return launch_encode(slab, g, d_tbl, s, tc);
+}
+bool encode_uses_ticket(uint64_t tiles, int k) {
+  return ECW_ENC_ASM && k >= 2 && ECW_TICKET_MIN_TILES > 0 && tiles >= ECW_TICKET_MIN_TILES;
 }
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes, int nblocks,
-                              uint64_t len, uint64_t seed, int s0, int b0, hipStream_t s) {
+                              uint64_t len, uint64_t piece, uint64_t pstride, uint64_t offset, uint64_t seed,
+                              int s0, int b0, hipStream_t s) {
   if (stripes <= 0 || nblocks <= 0 || len == 0) return hipSuccess;
-  const uint64_t npair = ((len + 7) / 8 + 1) / 2;
+  if (piece == 0 || offset % 16 || (piece < len && piece % 16)) return hipErrorInvalidValue;
+  const uint64_t npair = (len + 15) / 16;
   uint64_t gx = (npair + kBlock - 1) / kBlock;
   if (gx > 1024) gx = 1024;
   const int rows = stripes * nblocks;
   const dim3 grid(static_cast<unsigned>(gx), static_cast<unsigned>(rows < 65535 ? rows : 65535));
+  (void)hipGetLastError();  // report this launch's error, not an earlier one
   hipLaunchKernelGGL(fill_kernel, grid, dim3(kBlock), 0, s, dst, bstride, sstride, stripes, nblocks, len,
-                     seed, s0, b0);
+                     piece, pstride, offset, seed, s0, b0);
   return hipGetLastError();
 }
 

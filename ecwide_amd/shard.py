@@ -51,6 +51,33 @@ def weak_shard(per_rank: int, rank: int) -> tuple:
     return rank * per_rank, per_rank
 
 
+def hbm_fill_block_mib(free_bytes: int, k: int, parity_num: int, stripes: int, frac: float = 0.97) -> int:
+    """Block size (whole MiB) at which `stripes` stripes of k + parity_num
+    blocks (+ 4 KiB padding per block) and a one-block-per-stripe repair
+    output fit in `frac` of `free_bytes` (BASELINE configs[3])."""
+    per_mib = stripes * ((k + parity_num) * ((1 << 20) + 4096) + (1 << 20))
+    return int(frac * free_bytes) // per_mib
+
+
+def plan_rank(stripes_total: int, block_bytes: int, world: int, rank: int, strong: bool,
+              per_rank: int = 0, align: int = 4096) -> dict:
+    """This rank's share of a batch (no data moves between ranks).
+
+    * weak: `per_rank` stripes of its own (ids rank * per_rank ...);
+    * strong: a contiguous range of the `stripes_total` stripes;
+    * strong with fewer stripes than ranks: byte columns [col_offset,
+      col_offset + block_bytes) of every stripe (column_shard, `align`-aligned).
+    Returns {s0, stripes, block_bytes, col_offset, columns}."""
+    if not strong:
+        s0, n = weak_shard(per_rank, rank)
+        return dict(s0=s0, stripes=n, block_bytes=block_bytes, col_offset=0, columns=False)
+    if stripes_total < world:
+        off, n = column_shard(block_bytes, world, rank, align=align)
+        return dict(s0=0, stripes=stripes_total, block_bytes=n, col_offset=off, columns=True)
+    s0, n = stripe_shard(stripes_total, world, rank)
+    return dict(s0=s0, stripes=n, block_bytes=block_bytes, col_offset=0, columns=False)
+
+
 def max_over_ranks(value: float, device=None) -> float:
     import torch
     import torch.distributed as dist

@@ -14,7 +14,8 @@ stripes. Two layouts:
   after it. Each (stripe, piece) is encoded as an independent stripe of
   ``chunk`` bytes (ecw_encode_batch_split_dev); repair writes the rebuilt
   block contiguously. Measured faster for the encode's 128-read / 8-write
-  byte mix.
+  byte mix. ``fill_random`` writes the same block bytes
+  in both layouts, so a tiled slab's parities equal the block slab's.
 """
 from __future__ import annotations
 
@@ -93,18 +94,20 @@ class StripeSlab:
         return [self.block(s, k + i) for i in range(self.codec.parityNum)]
 
     # operations -------------------------------------------------------------
-    def fill_random(self, seed: int, s0: int = 0) -> None:
-        """Synthetic data blocks (ecwide.h counter PRNG), stripe ids s0..
-        (tiled layout: unit u = stripe * pieces + piece is PRNG stripe s0 * pieces + u)."""
+    def fill_random(self, seed: int, s0: int = 0, col_offset: int = 0) -> None:
+        """Synthetic data blocks (ecwide.h counter PRNG), stripe ids s0..: data
+        block j of stripe s holds bytes [col_offset, col_offset + len) of the
+        generator stream (seed, s0 + s, j) in both layouts, so a block reads the
+        same through block() whatever the layout (col_offset: this slab holds a
+        column slice of longer blocks, e.g. one rank's shard.column_shard)."""
         k = self.codec.encodeDataNum
         if self.layout == "tiled":
-            _check(lib.ecw_fill_random_dev(self.codec.device, c_void_p(self.base), self.chunk, self.unit_stride,
-                                           self.units, k, self.chunk, seed, s0 * self.pieces, 0, _stream()),
-                   "fill_random")
-            return
-        _check(lib.ecw_fill_random_dev(self.codec.device, c_void_p(self.base), self.block_stride,
-                                       self.stripe_stride, self.stripes, k, self.len,
-                                       seed, s0, 0, _stream()), "fill_random")
+            ch = self.chunk
+            args = (ch, self.pieces * self.unit_stride, self.stripes, k, self.len, ch, self.unit_stride)
+        else:
+            args = (self.block_stride, self.stripe_stride, self.stripes, k, self.len, max(16, self.out_stride), 0)
+        _check(lib.ecw_fill_random_pieces_dev(self.codec.device, c_void_p(self.base), *args, col_offset, seed, s0, 0,
+                                              _stream()), "fill_random")
 
     def encode(self, stream=None) -> None:
         st = stream if stream is not None else _stream()

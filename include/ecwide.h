@@ -257,6 +257,15 @@ int ecw_repair_sources(const ecw_codec* codec, int lost_block, int* out_blocks, 
 int ecw_fill_random_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride,
                         int stripes, int nblocks, size_t len, uint64_t seed, int s0, int b0,
                         void* stream);
+/* The same generator for blocks stored in column pieces (the tiled slab) or
+ * as a column slice (a column-sharded rank): byte i of a block is byte
+ * `offset` + i of its stream and lands at
+ *   d_dst + s*stripe_stride + b*block_stride + (i / piece)*piece_stride + i % piece,
+ * so a block holds the same bytes in every layout. piece, piece_stride and
+ * offset are multiples of 16 (piece >= len: one contiguous block). */
+int ecw_fill_random_pieces_dev(int device, uint8_t* d_dst, size_t block_stride, size_t stripe_stride,
+                               int stripes, int nblocks, size_t len, size_t piece, size_t piece_stride,
+                               size_t offset, uint64_t seed, int s0, int b0, void* stream);
 
 #ifdef __cplusplus
 }

@@ -74,6 +74,7 @@ class Oracle:
         L.orc_nc_partial_decode.argtypes = [c_void_p, _u8pp, _u8p, c_int]
         L.orc_nc_xor_intermediate.argtypes = [c_void_p, _u8pp, _u8pp, c_int, c_int]
         L.orc_fill_random.argtypes = [_u8p, c_size_t, c_uint64, c_uint32, c_uint32]
+        L.orc_fill_random_at.argtypes = [_u8p, c_size_t, c_size_t, c_uint64, c_uint32, c_uint32]
         L.orc_xor_blocks.argtypes = [_u8pp, c_int, _u8p, c_size_t]
         L.orc_have_avx2.restype = c_int
 
@@ -107,9 +108,12 @@ class Oracle:
         f(ln, len(src), rows, tbls.ctypes.data_as(_u8p), _ptrs(src), _ptrs(out))
         return out
 
-    def fill(self, length: int, seed: int, stripe: int, block: int) -> np.ndarray:
+    def fill(self, length: int, seed: int, stripe: int, block: int, offset: int = 0) -> np.ndarray:
+        """Bytes [offset, offset + length) of block `block` of stripe `stripe`
+        (ecwide.h generator; offset a multiple of 8)."""
+        assert offset % 8 == 0
         a = np.zeros(length, np.uint8)
-        self.L.orc_fill_random(a.ctypes.data_as(_u8p), length, seed, stripe, block)
+        self.L.orc_fill_random_at(a.ctypes.data_as(_u8p), offset, length, seed, stripe, block)
         return a
 
     def xor_blocks(self, src: list) -> np.ndarray:

@@ -421,18 +421,24 @@ static uint64_t mix64(uint64_t z) {
   return z;
 }
 
-void orc_fill_random(uint8_t* dst, size_t len, uint64_t seed, uint32_t stripe, uint32_t block) {
+/* bytes [off, off + len) of the stream of (seed, stripe, block); off % 8 == 0 */
+void orc_fill_random_at(uint8_t* dst, size_t off, size_t len, uint64_t seed, uint32_t stripe, uint32_t block) {
   const uint64_t G = 0x9E3779B97F4A7C15ull;
   uint64_t key = mix64(seed + G * (1ull + (uint64_t)stripe * 65536ull + block));
+  const uint64_t w0 = off / 8;
   size_t nw = len / 8;
   for (size_t w = 0; w < nw; ++w) {
-    uint64_t v = mix64(key + (uint64_t)w * G);
+    uint64_t v = mix64(key + (w0 + w) * G);
     memcpy(dst + 8 * w, &v, 8);
   }
   if (len % 8) {
-    uint64_t v = mix64(key + (uint64_t)nw * G);
+    uint64_t v = mix64(key + (w0 + nw) * G);
     memcpy(dst + 8 * nw, &v, len % 8);
   }
+}
+
+void orc_fill_random(uint8_t* dst, size_t len, uint64_t seed, uint32_t stripe, uint32_t block) {
+  orc_fill_random_at(dst, 0, len, seed, stripe, block);
 }
 
 /* XOR of n blocks (flat CL repair) */

@@ -1,0 +1,62 @@
+"""The N>1 path with the product on the GPU: two torch.distributed.run ranks
+(sharing the box's GPU, gloo) each encode and repair their share of a batch
+with StripeSlab (tests/mp_rank_worker.py); the union of their outputs equals
+the single-process encode of the whole batch, for stripe sharding and for the
+byte-column fallback."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("mode", ["stripes", "columns"])
+def test_two_ranks_union_equals_single_process(tmp_path, mode):
+    import torch
+
+    import ecwide_amd as E
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", f"--master-port={_port()}", os.path.join(HERE, "mp_rank_worker.py"),
+           str(tmp_path), mode]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stderr[-3000:]
+    k, m, r, B, chunk, seed = 32, 3, 11, 4 * 8192, 8192, 61
+    total = 5 if mode == "stripes" else 1
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=total, block_bytes=B, layout="tiled", chunk=chunk)
+    slab.fill_random(seed=seed)
+    slab.encode()
+    torch.cuda.synchronize()
+    want = {s: np.stack([p.cpu().numpy() for p in slab.parity(s)]) for s in range(total)}
+    d0 = {s: slab.block(s, 0).cpu().numpy() for s in range(total)}
+    got_par = {s: np.zeros_like(want[s]) for s in range(total)}
+    got_rep = {s: np.zeros(B, np.uint8) for s in range(total)}
+    covered = {s: np.zeros(B, bool) for s in range(total)}
+    for rank in range(2):
+        z = np.load(tmp_path / f"rank{rank}.npz")
+        s0, off, n = int(z["s0"]), int(z["col_offset"]), int(z["stripes"])
+        for i in range(n):
+            par, rep = z[f"par{i}"], z[f"rep{i}"]
+            w = rep.size
+            assert not covered[s0 + i][off:off + w].any(), "a column or stripe owned twice"
+            covered[s0 + i][off:off + w] = True
+            got_par[s0 + i][:, off:off + w] = par
+            got_rep[s0 + i][off:off + w] = rep
+    for s in range(total):
+        assert covered[s].all(), (mode, s)
+        assert np.array_equal(got_par[s], want[s]), (mode, s)
+        assert np.array_equal(got_rep[s], d0[s]), (mode, s)

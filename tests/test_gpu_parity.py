@@ -194,7 +194,7 @@ def test_tiled_slab_encode_repair(E, torch, orc, k, m, r, B, S, chunk):
         par = [p.cpu().numpy() for p in slab.parity(s)]
         for piece in range(slab.pieces):
             sl = slice(piece * chunk, (piece + 1) * chunk)
-            assert np.array_equal(data[0][sl], orc.fill(chunk, 71, s * slab.pieces + piece, 0))
+            assert np.array_equal(data[0][sl], orc.fill(chunk, 71, s, 0, piece * chunk))
             want = oc.encode([d[sl] for d in data])
             for i, w in enumerate(want):
                 assert np.array_equal(par[i][sl], w), (s, piece, i)
@@ -241,29 +241,120 @@ def test_repair_group_sizes(E, torch, k, r, layout):
             assert torch.equal(out[s * o:s * o + B], slab.block(s, lost)), (lost, s)
 
 
-def test_ticket_launch_matches_windows(E, torch, orc):
+@pytest.mark.parametrize("k,m,r,B,S,layout,local", [
+    (4, 2, 2, 256 << 20, 4, "blocks", "xor"),      # 1 global row pass, parked locals
+    (4, 6, 2, 256 << 20, 4, "blocks", "xor"),      # 5-8 rows: the u64-entry (NW=2) tile
+    (12, 3, 2, 64 << 20, 16, "blocks", "xor"),     # 6 groups: locals not parked
+    (4, 2, 2, 256 << 20, 4, "blocks", "literal"),  # ECWide-C literal mode: zero L blocks
+    (8, 3, 4, 128 << 20, 8, "tiled", "xor"),       # the bench's split (tiled) layout, 262,144 tiles
+])
+def test_ticket_launch_matches_windows(E, torch, orc, k, m, r, B, S, layout, local):
     """A slab of >= 262,144 column tiles is encoded by one ticket-ordered
     launch (ecw_kernels.hip launch_encode); each stripe encoded on its own
-    (65,536 tiles: the launch-window path) must give the same parities, and a
-    column sample must match the oracle."""
-    k, m, r, B, S = 4, 2, 2, 256 << 20, 4
-    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
-    slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+    (pointer mode, < 262,144 tiles: the launch-window path) must give the same
+    parities, and the last column window (claimed last by the ticket order)
+    must match the oracle. A second encode of the slab on the same stream
+    reuses the counter (ticket base carried over) and must give the same bytes."""
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
+    kw = {"layout": "tiled", "chunk": 8192} if layout == "tiled" else {}
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, **kw)
     assert slab.encode_launches() == 1
     slab.fill_random(seed=404)
     slab.encode()
     np_ = c.parityNum
+    W = 8192
+    oc = orc.codec("C", k, m, r, W)
+    first = [[p[-W:].clone() for p in slab.parity(s)] for s in (0, S - 1)]
     pbuf = torch.empty((np_, B), dtype=torch.uint8, device="cuda")
-    oc = orc.codec("C", k, m, r, 8192)
     for s in (0, S - 1):
         c.encodeData([slab.block(s, j) for j in range(k)], [pbuf[i] for i in range(np_)])
         torch.cuda.synchronize()
         for i, p in enumerate(slab.parity(s)):
             assert torch.equal(p, pbuf[i]), (s, i)
-        off = B - 8192  # last column tile: claimed last by the ticket order
-        want = oc.encode([slab.block(s, j)[off:].cpu().numpy() for j in range(k)])
+        want = oc.encode([orc.fill(W, 404, s, j, B - W) for j in range(k)], literal=local == "literal")
         for i, w in enumerate(want):
-            assert np.array_equal(pbuf[i][off:].cpu().numpy(), w), (s, i)
+            assert np.array_equal(pbuf[i][B - W:].cpu().numpy(), w), (s, i)
+    if layout == "tiled":
+        slab.buf[slab.parity_offset:].zero_()
+    else:
+        for p in slab.parity(0) + slab.parity(S - 1):
+            p.zero_()
+    slab.encode()  # second launch on the same counter
+    torch.cuda.synchronize()
+    for n, s in enumerate((0, S - 1)):
+        for i, p in enumerate(slab.parity(s)):
+            assert torch.equal(p[-W:], first[n][i]), ("second encode", s, i)
+
+
+def test_full_size_tiled_bench_path(E, torch, manifest):
+    """The bench's timed bytes at the bench's size: tiled slab, CL(128, 27, 3),
+    64 MiB blocks, 8 stripes, seed 103. Stripe 0 is the stripe of manifest
+    'cfg3_full' (digests from the reference's ISA-L build): every parity and
+    the D0 repair match its SHA-256; every stripe's parities equal the block
+    slab's encode of the same bytes and every D0 repair equals D0."""
+    e = next(x for x in manifest["full"] if x["name"] == "cfg3_full")
+    k, m, r, B, S = e["k"], e["m"], e["r"], e["len"], 8
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    tiled = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled", chunk=8192)
+    tiled.fill_random(seed=e["seed"])
+    tiled.encode()
+    out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
+    tiled.repair(0, out)
+    torch.cuda.synchronize()
+    assert [sha(p.cpu().numpy()) for p in tiled.parity(0)] == e["parity_sha256"]
+    assert sha(out[:B].cpu().numpy()) == e["repair_d0_sha256"]
+    blocks = E.StripeSlab(c, stripes=S, block_bytes=B)
+    blocks.fill_random(seed=e["seed"])
+    blocks.encode()
+    torch.cuda.synchronize()
+    for s in range(S):
+        assert torch.equal(out[s * B:(s + 1) * B], tiled.block(s, 0)), s
+        for i, (a, b) in enumerate(zip(tiled.parity(s), blocks.parity(s))):
+            assert torch.equal(a, b), (s, i)
+    del tiled, blocks, out
+    torch.cuda.empty_cache()
+
+
+def test_hbm_filling_batch_configs3(E, torch, orc):
+    """BASELINE configs[3] as the bench runs it (bench.py --hbm-fill): 256
+    stripes, block size sized from free HBM (shard.hbm_fill_block_mib), tiled
+    slab, ONE ticket-ordered launch. Oracle windows at the first, middle and
+    last column piece of the first, middle and last stripe; stripes 0 and 255
+    re-encoded alone (launch-window path) equal; every stripe's D0 repair == D0."""
+    from ecwide_amd.shard import hbm_fill_block_mib
+
+    k, m, r, S, W, seed = 128, 3, 27, 256, 8192, 103
+    torch.cuda.empty_cache()
+    free = torch.cuda.mem_get_info()[0]
+    mib = hbm_fill_block_mib(free, k, m + 5, S)
+    assert mib >= 1, free
+    B = mib << 20
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled", chunk=W)
+    assert slab.encode_launches() == 1
+    out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
+    slab.fill_random(seed=seed)
+    slab.encode()
+    slab.repair(0, out)
+    torch.cuda.synchronize()
+    oc = orc.codec("C", k, m, r, W)
+    for s in (0, S // 2, S - 1):
+        par = slab.parity(s)
+        for off in (0, B // 2, B - W):
+            want = oc.encode([orc.fill(W, seed, s, j, off) for j in range(k)])
+            for i, w in enumerate(want):
+                assert np.array_equal(par[i][off:off + W].cpu().numpy(), w), (s, off, i)
+    for s in range(S):
+        assert torch.equal(out[s * B:(s + 1) * B], slab.block(s, 0)), s
+    del out
+    pbuf = torch.empty((c.parityNum, B), dtype=torch.uint8, device="cuda")
+    for s in (0, S - 1):
+        c.encodeData([slab.block(s, j) for j in range(k)], [pbuf[i] for i in range(c.parityNum)])
+        torch.cuda.synchronize()
+        for i, p in enumerate(slab.parity(s)):
+            assert torch.equal(p, pbuf[i]), (s, i)
+    del slab, pbuf
+    torch.cuda.empty_cache()
 
 
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
@@ -337,6 +428,24 @@ def test_fill_kernel_matches_oracle(E, torch, orc):
     for st in range(3):
         for j in range(10):
             assert np.array_equal(slab.block(st, j).cpu().numpy(), orc.fill(5000, 123, 4 + st, j)), (st, j)
+
+
+@pytest.mark.parametrize("chunk,col_offset", [(8192, 0), (4096, 0), (8192, 3 * 8192)])
+def test_fill_same_bytes_in_every_layout(E, torch, orc, chunk, col_offset):
+    """The tiled slab's blocks hold exactly the block slab's bytes (the PRNG is
+    keyed by stripe, block and byte offset, scattered by column piece), also
+    for a column slice starting at col_offset (a column-sharded rank)."""
+    k, B = 12, 4 * 8192
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, 2, 5, B), 1, False)
+    blocks = E.StripeSlab(c, stripes=3, block_bytes=B)
+    tiled = E.StripeSlab(c, stripes=3, block_bytes=B, layout="tiled", chunk=chunk)
+    blocks.fill_random(seed=55, s0=2, col_offset=col_offset)
+    tiled.fill_random(seed=55, s0=2, col_offset=col_offset)
+    torch.cuda.synchronize()
+    for st in range(3):
+        for j in range(k):
+            assert torch.equal(tiled.block(st, j), blocks.block(st, j)), (st, j)
+            assert np.array_equal(tiled.block(st, j).cpu().numpy(), orc.fill(B, 55, 2 + st, j, col_offset)), (st, j)
 
 
 @pytest.mark.parametrize("k,m,r,B,S", [(32, 3, 11, 1 << 20, 2), (32, 2, 8, (1 << 18) + 48, 3),

@@ -143,3 +143,68 @@ def test_two_rank_gloo_partition():
     for s in range(total):
         par = oc.encode([orc.fill(1024, 5, s, j) for j in range(12)])
         assert merged[s] == hashlib.sha256(b"".join(p.tobytes() for p in par)).hexdigest()
+
+
+# ---- bench.py's own rank orchestration (no GPU: --dry-run) -------------------
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench(*args, env=None):
+    import json
+    import subprocess
+    import sys
+
+    e = {x: v for x, v in os.environ.items() if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    e.update(env or {})
+    p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
+                       timeout=240, env=e)
+    return p, (json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None)
+
+
+def test_bench_gpus2_launches_two_ranks_configs4_default():
+    """`bench.py --gpus 2` (no torch.distributed.run around it) starts 2 ranks
+    itself; the N>1 default is configs[4]: the 256-stripe HBM-filling batch
+    (B sized so the whole batch fits one GPU, same B on every rank) split by
+    stripe; the reported time is the max over ranks."""
+    p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-free-gib", "287")
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["hbm_fill"]
+    assert line["stripes_total"] == 256 and line["block_bytes"] == 8 << 20
+    sh = line["shares"]
+    assert [(x["s0"], x["stripes"]) for x in sh] == [(0, 128), (128, 128)]
+    assert {x["block_bytes"] for x in sh} == {8 << 20}
+    assert line["el_max"] == max(line["rank_seconds"]) and len(line["rank_seconds"]) == 2
+
+
+def test_bench_dry_run_weak_and_column_modes():
+    p, line = _bench("--gpus", "2", "--dry-run", "--weak")
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert line["scaling"] == "weak" and line["stripes_total"] == 16
+    assert [(x["s0"], x["stripes"]) for x in line["shares"]] == [(0, 8), (8, 8)]
+    # fewer stripes than ranks: byte columns of every stripe, aligned to the tiled piece
+    p, line = _bench("--gpus", "3", "--dry-run", "--strong", "--stripes", "1")
+    assert p.returncode == 0, p.stderr[-2000:]
+    sh = line["shares"]
+    assert sh[0]["col_offset"] == 0 and all(x["col_offset"] % 8192 == 0 for x in sh)
+    assert sum(x["block_bytes"] for x in sh) == 64 << 20
+    for a, b in zip(sh, sh[1:]):
+        assert a["col_offset"] + a["block_bytes"] == b["col_offset"]
+
+
+def test_bench_rejects_world_size_mismatch():
+    p, _ = _bench("--gpus", "2", "--dry-run", env={"WORLD_SIZE": "3", "RANK": "0", "LOCAL_RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE=3" in p.stderr
+
+
+def test_plan_rank_and_hbm_fill_sizing():
+    from ecwide_amd.shard import hbm_fill_block_mib, plan_rank
+
+    # 288 GiB HBM, k=128 + 8 parities, 256 stripes: 8 MiB blocks (272 GiB slab)
+    assert hbm_fill_block_mib(287 << 30, 128, 8, 256) == 8
+    assert hbm_fill_block_mib(1 << 30, 128, 8, 256) == 0
+    for world in (1, 2, 4, 8):
+        got = [plan_rank(256, 8 << 20, world, r, strong=True) for r in range(world)]
+        assert sum(g["stripes"] for g in got) == 256 and all(not g["columns"] for g in got)
+        assert [g["s0"] for g in got] == [256 // world * r for r in range(world)]
+    w = plan_rank(8, 1 << 26, 4, 3, strong=False, per_rank=8)
+    assert (w["s0"], w["stripes"]) == (24, 8)
