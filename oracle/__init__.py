@@ -6,7 +6,8 @@ ctypes bindings for two CPU checkers:
   (oracle/ecw_oracle.c; every function there cites the reference file:line
   it restates);
 * ``_ref/libisal_base.so`` — the reference's own arithmetic: ISA-L 2.14.0
-  ``erasure_code/ec_base.c`` compiled unmodified from the tarball that
+  ``erasure_code/ec_base.c`` + ``ec_highlevel_func.c`` (``ec_init_tables``)
+  compiled unmodified from the tarball that
   ECWide-H bundles (oracle/Makefile). Present wherever ``build()`` ran in a
   container that has /root/reference; the prebuilt .so travels to the GPU box.
 
@@ -191,8 +192,11 @@ class RefIsal:
     def __init__(self, path: str = REF_PATH):
         if not os.path.exists(path):
             raise FileNotFoundError(path)
-        L = ctypes.CDLL(path)
+        # lazy binding: the SIMD dispatchers of ec_highlevel_func.c reference
+        # NASM kernels that are not built (oracle/Makefile); never called here
+        L = ctypes.CDLL(path, mode=os.RTLD_LAZY)
         self.L = L
+        L.ec_init_tables.argtypes = [c_int, c_int, _u8p, _u8p]
         L.gf_mul.restype = c_uint8
         L.gf_mul.argtypes = [c_uint8, c_uint8]
         L.gf_inv.restype = c_uint8
@@ -213,14 +217,11 @@ class RefIsal:
         return a.reshape(n, k)
 
     def init_tables(self, k: int, rows: int, a: np.ndarray) -> np.ndarray:
-        # ec_init_tables (isal:erasure_code/ec_highlevel_func.c:33-43) is this
-        # loop over gf_vect_mul_init; that file also references the SIMD
-        # kernels (unassemblable without nasm), so the loop is restated here.
+        """ec_init_tables (isal:erasure_code/ec_highlevel_func.c:33-43), the
+        reference's own function."""
         a = np.ascontiguousarray(a, np.uint8).reshape(-1)
         g = np.zeros(32 * k * rows, np.uint8)
-        base = g.ctypes.data
-        for i in range(rows * k):
-            self.L.gf_vect_mul_init(int(a[i]), ctypes.cast(base + 32 * i, _u8p))
+        self.L.ec_init_tables(k, rows, a.ctypes.data_as(_u8p), g.ctypes.data_as(_u8p))
         return g
 
     def encode_data(self, tbls: np.ndarray, src: list, rows: int):
