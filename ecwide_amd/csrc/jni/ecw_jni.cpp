@@ -41,8 +41,15 @@ namespace {
 // type, k, m, r, node, multinode, local mode, chunk
 using Key = std::tuple<char, int, int, int, int, int, int, long long>;
 
+// codecs are immutable after creation: one per parameter set for the life of
+// the library, released when it is unloaded
+struct Codecs : std::map<Key, ecw_codec*> {
+  ~Codecs() {
+    for (auto& kv : *this) ecw_codec_destroy(kv.second);
+  }
+};
 std::mutex g_mu;
-std::map<Key, ecw_codec*> g_codecs;
+Codecs g_codecs;
 std::atomic<bool> g_xori_called{false};
 
 void throw_java(JNIEnv* e, const char* cls, const std::string& msg) {
