@@ -45,11 +45,13 @@ def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1,
                     help="ranks (one per GPU); without a torch.distributed.run environment bench.py launches them")
-    ap.add_argument("--layout", choices=["blocks", "tiled"], default="tiled",
+    ap.add_argument("--layout", choices=["blocks", "split", "tiled"], default="tiled",
                     help="slab layout in HBM (ecwide_amd/slab.py): tiled (default; each --chunk-kib column piece "
-                         "of the k data blocks contiguous, parities apart) or whole blocks at a padded stride")
+                         "of the k data blocks contiguous, parities apart), split (whole blocks, parity blocks in "
+                         "a region of their own) or blocks (whole blocks, [D.., G.., L..] per stripe)")
     ap.add_argument("--other-layout-steps", type=int, default=5,
-                    help="N=1: also time this many steps on the other layout and report them in the line (0 = off)")
+                    help="N=1: also time this many steps with whole blocks (split slab, pointer mode) and report "
+                         "them in the line (0 = off)")
     ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
     ap.add_argument("--unit-pad", type=int, default=0, help="tiled layout: padding after each piece run (bytes)")
     ap.add_argument("--steps", type=int, default=20)
@@ -258,6 +260,7 @@ def cpu_baseline(args, k, m, r, B):
 
     res = {}
     allc = host_threads()
+    run(allc)  # warm: fault in the output pages outside the timing
     for threads in sorted({1, allc}):
         n, t0 = 0, time.perf_counter()
         while True:
@@ -325,6 +328,49 @@ def verify(args, slab, out, pl, k, m, r) -> dict:
                 return dict(res, ok=False, failed="stripe 0 vs manifest cfg3_full digests")
             res["digests"] = True
     return dict(res, ok=True)
+
+
+def other_layouts(args, E, codec, S, B, s0, out, enc_bytes, rep_bytes, dev) -> dict:
+    """Encode / repair rates of the bench workload in whole-block layouts."""
+    import torch
+
+    n2 = args.other_layout_steps
+    res = {}
+
+    def timed(run, nbytes):
+        run()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(n2):
+            run()
+        e1.record()
+        torch.cuda.synchronize()
+        return round(nbytes * n2 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 2)
+
+    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=dev, layout="split")
+    slab.fill_random(seed=args.seed, s0=s0)
+    enc = timed(slab.encode, enc_bytes)
+    rep = timed(lambda: slab.repair(0, out), rep_bytes)
+    res["split"] = {"layout": "split: whole blocks (stride B + 4 KiB), data blocks of all stripes then their "
+                              "parity blocks", "steps": n2, "encode_GBps": enc, "repair_GBps": rep,
+                    "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
+    del slab
+    torch.cuda.empty_cache()
+    # pointer mode: every block its own allocation (data blocks first, then parities)
+    k, np_ = codec.encodeDataNum, codec.parityNum
+    data = [[torch.empty(B, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(k)] for _ in range(S)]
+    par = [[torch.empty(B, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(np_)] for _ in range(S)]
+    gen = torch.Generator(device=f"cuda:{dev}").manual_seed(args.seed)
+    for blocks in data:
+        for blk in blocks:
+            blk.random_(0, 256, generator=gen)
+    batch = E.BlockBatch(codec, data, par)
+    enc = timed(batch.encode, enc_bytes)
+    res["pointer"] = {"layout": f"pointer mode: {S * (k + np_)} separately allocated {B >> 20} MiB blocks, one "
+                                f"ecw_encode_ptrs_dev launch over the {S} stripes", "steps": n2, "encode_GBps": enc,
+                      "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
+    return res
 
 
 # ---- the PCIe-inclusive rate --------------------------------------------------
@@ -528,9 +574,10 @@ def main():
             "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B,
             "stripes_per_gpu": S, "stripes_total": S_total, "seed": args.seed,
             "parallelism": f"stripe-partitioned x{d.world} (no collectives on the data path)",
-            "layout": ("blocks (each block contiguous, block stride B + 4 KiB)" if args.layout == "blocks" else
-                       f"tiled ({args.chunk_kib} KiB column pieces: the k data pieces contiguous, "
-                       f"parities in their own region)"),
+            "layout": {"blocks": "blocks (each block contiguous, block stride B + 4 KiB, [D.., G.., L..] per stripe)",
+                       "split": "split (each block contiguous, block stride B + 4 KiB, parity blocks in their own "
+                                "region)"}.get(args.layout, f"tiled ({args.chunk_kib} KiB column pieces: the k data "
+                                                            f"pieces contiguous, parities in their own region)"),
             "encode_bytes_per_step_per_gpu": enc_bytes,
             "repair_bytes_per_step_per_gpu": rep_bytes,
         },
@@ -563,42 +610,13 @@ def main():
         line["verify"] = {key: vres[key] for key in ("windows", "repairs", "digests")} | (
             {"failed": vres["failed"]} if not vres["ok"] else {})
     if d.world == 1 and args.other_layout_steps > 0 and not pl["hbm_fill"]:
-        # the same workload on the other slab layout, for comparison (not `value`)
-        other = "blocks" if args.layout == "tiled" else "tiled"
+        # the same workload with whole contiguous blocks (not `value`): the split
+        # slab (data blocks, then parity blocks, ecw_*_batch_split_dev) and the
+        # reference's per-block pointer interface on separately allocated blocks
+        # (one ecw_encode_ptrs_dev launch for all stripes)
         del slab
         torch.cuda.empty_cache()
-        slab2 = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=other,
-                             chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
-        slab2.fill_random(seed=args.seed, s0=s0)
-        n2 = args.other_layout_steps
-        out2 = out if out.numel() >= S * slab2.out_stride else torch.empty(S * slab2.out_stride, dtype=torch.uint8,
-                                                                           device=f"cuda:{d.dev}")
-        for _ in range(2):
-            slab2.encode()
-            slab2.repair(0, out2)
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(n2):
-            slab2.encode()
-            slab2.repair(0, out2)
-        torch.cuda.synchronize()
-        el2 = time.perf_counter() - t0
-        ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
-        ev[0].record()
-        for _ in range(n2):
-            slab2.encode()
-        ev[1].record()
-        for _ in range(n2):
-            slab2.repair(0, out2)
-        ev[2].record()
-        torch.cuda.synchronize()
-        line["other_layout"] = {
-            "layout": other, "steps": n2,
-            "value": round(step_bytes * n2 / el2 / 1e9, 2),
-            "encode_GBps": round(enc_bytes * n2 / (ev[0].elapsed_time(ev[1]) * 1e-3) / 1e9, 2),
-            "repair_GBps": round(rep_bytes * n2 / (ev[1].elapsed_time(ev[2]) * 1e-3) / 1e9, 2),
-        }
-        del slab2
+        line["other_layout"] = other_layouts(args, E, codec, S, B, s0, out, enc_bytes, rep_bytes, d.dev)
         torch.cuda.empty_cache()
     if d.world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)

@@ -76,6 +76,7 @@ SIGNATURES = {
     "ecw_encode_stripes": (c_int, [c_void_p, c_int, _pp, _pp, c_size_t]),
     "ecw_matrix_codec_create": (c_int, [_u8p, c_int, c_int, c_int, POINTER(c_void_p)]),
     "ecw_encode_dev": (c_int, [c_void_p, _pp, _pp, c_size_t, c_void_p]),
+    "ecw_encode_ptrs_dev": (c_int, [c_void_p, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ecw_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
     "ecw_partial_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
     "ecw_xor_intermediate_dev": (c_int, [c_void_p, _pp, _pp, c_size_t, c_void_p]),

@@ -260,11 +260,60 @@ class NativeCodec:
             arr[i] = _addr(b) if b is not None else None
         _check(lib.ecw_repair(self._h, arr, lost_block, _addr(out), n), "repairBlock")
 
+    def encodeStripes(self, data, parity, length=None) -> None:
+        """Encode a batch of stripes: data[s] / parity[s] are stripe s's block
+        lists (the encodeData convention, NativeCodec.cc:158-166). HBM blocks
+        go through ONE launch for the whole batch (ecw_encode_ptrs_dev, device
+        pointer tables); host blocks through ecw_encode_stripes."""
+        if not data:
+            return
+        if _on_device([b for st in data for b in st] + [b for st in parity for b in st]):
+            BlockBatch(self, data, parity, length).encode()
+            return
+        k, np_ = self.encodeDataNum, self.parityNum
+        flat_d = [b for st in data for b in list(st)[:k]]
+        flat_p = [b for st in parity for b in list(st)[:np_]]
+        if len(flat_d) != k * len(data) or len(flat_p) != np_ * len(data):
+            raise ValueError(f"every stripe needs {k} data and {np_} parity blocks")
+        n = self._len(flat_d + flat_p, length)
+        _check(lib.ecw_encode_stripes(self._h, len(data), _parr(flat_d), _parr(flat_p), n), "encodeStripes")
+
     # -- CL repair fan-in (ClMetadataManager.java:137-257, flattened) --------
     def repairSources(self, lost_block: int) -> list:
         buf = (c_int * 256)()
         n = _check(lib.ecw_repair_sources(self._h, lost_block, buf, 256), "repairSources")
         return list(buf[:n])
+
+
+class BlockBatch:
+    """A batch of stripes whose blocks sit anywhere in HBM (separate
+    allocations, the reference's per-block pointers): the block pointers are
+    uploaded once as device tables, and every encode() of the batch is ONE
+    kernel launch over all stripes (ecw_encode_ptrs_dev)."""
+
+    def __init__(self, codec: NativeCodec, data, parity, length=None):
+        import torch
+
+        k, np_ = codec.encodeDataNum, codec.parityNum
+        if len(data) != len(parity) or any(len(d) < k for d in data) or any(len(p) < np_ for p in parity):
+            raise ValueError(f"every stripe needs {k} data and {np_} parity blocks")
+        self.codec, self.stripes = codec, len(data)
+        blocks = [b for st in data for b in list(st)[:k]] + [b for st in parity for b in list(st)[:np_]]
+        if not _on_device(blocks):
+            raise ValueError("BlockBatch holds HBM blocks (torch CUDA tensors)")
+        self.len = codec._len(blocks, length)
+        dev = blocks[0].device
+        self._keep = blocks  # the blocks stay alive as long as their pointers are in the tables
+        self.dtab = torch.tensor([_addr(b) for st in data for b in list(st)[:k]], dtype=torch.int64, device=dev)
+        self.ptab = torch.tensor([_addr(b) for st in parity for b in list(st)[:np_]], dtype=torch.int64, device=dev)
+
+    def encode(self, stream=None) -> None:
+        _check(lib.ecw_encode_ptrs_dev(self.codec._h, self.stripes, c_void_p(self.dtab.data_ptr()),
+                                       c_void_p(self.ptab.data_ptr()), self.len,
+                                       stream if stream is not None else _stream()), "encodeStripes")
+
+    def encode_bytes(self) -> int:
+        return self.stripes * (self.codec.encodeDataNum + self.codec.parityNum) * self.len
 
 
 def xor_reduce(src, dst, length=None, device: int = 0) -> None:

@@ -298,6 +298,17 @@ int run_xor_ptr(const uint8_t* const* src, int n, uint8_t* dst, size_t len, hipS
 
 bool check_len(size_t len) { return len <= 0xFFFFFFF0ull; }
 
+// The `rows` blocks of `stripes` stripes at s * sstride + j * bstride, each
+// `len` bytes, never overlap: stripes one after another (stripe-major), or
+// the stripes interleaved inside every block (block-major: e.g. the column
+// pieces of one block-layout stripe taken as stripes of their own).
+bool disjoint_units(size_t bstride, size_t sstride, size_t rows, int stripes, size_t len) {
+  if (stripes <= 1 || len == 0) return true;
+  const size_t S = static_cast<size_t>(stripes);
+  if (sstride >= (rows - 1) * bstride + len) return true;
+  return sstride >= len && (rows <= 1 || bstride >= (S - 1) * sstride + len);
+}
+
 template <class P>
 bool all_aligned(P const* ptrs, int n) {
   for (int i = 0; i < n; ++i)
@@ -579,6 +590,48 @@ int ecw_encode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* const* d
   return run_encode(c, t, len, static_cast<hipStream_t>(stream));
 }
 
+int ecw_encode_ptrs_dev(ecw_codec* c, int stripes, const uint8_t* const* d_data_ptrs, uint8_t* const* d_parity_ptrs,
+                        size_t len, void* stream) {
+  if (!c || !d_data_ptrs || !d_parity_ptrs || stripes < 0 || !check_len(len)) return ECW_EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_data_ptrs) % 8 || reinterpret_cast<uintptr_t>(d_parity_ptrs) % 8)
+    return ECW_EALIGN;
+  const int k = c->k(), m = c->m(), ng = c->groups();
+  if (m < 1 && local_mode_of(c) != kLocalNone) return ECW_EUNSUPPORTED;  // locals ride in a global-row pass
+  if (len == 0 || stripes == 0 || m < 1) return ECW_OK;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    const int st = c->ensure_device();
+    if (st) return st;
+  }
+  DeviceGuard g(c->device);
+  if (!g.ok) return ECW_EDEVICE;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  EncodeGeom eg{};
+  eg.len = len;
+  eg.tiles = (len + kTileBytes - 1) / kTileBytes;
+  eg.stripes = stripes;
+  eg.k = k;
+  eg.r = c->has_local() ? c->r() : k;
+  eg.groups = ng;
+  eg.m = m;
+  const PtrTabRows rows{d_data_ptrs, d_parity_ptrs, c->info.parity_num};
+  const int npass = (m + kMaxPassRows - 1) / kMaxPassRows;
+  for (int q = 0; q < npass; ++q) {
+    eg.row0 = q * kMaxPassRows;
+    eg.nrows = std::min(kMaxPassRows, m - eg.row0);
+    eg.local_mode = q == 0 ? local_mode_of(c) : kLocalNone;
+    hipError_t e;
+    if (encode_uses_ticket(eg.tiles * static_cast<uint64_t>(stripes), k)) {
+      std::lock_guard<std::mutex> lk(c->ticket_mu);
+      e = launch_encode_tab(rows, eg, c->d_pass[q], s, c->ticket_for(s));
+    } else {
+      e = launch_encode_tab(rows, eg, c->d_pass[q], s, nullptr);
+    }
+    if (e != hipSuccess) return ECW_EDEVICE;
+  }
+  return ECW_OK;
+}
+
 int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* d_dst, size_t len, void* stream) {
   if (!d_src || !d_dst || n < 1 || n > kMaxSrc || !check_len(len)) return ECW_EINVAL;
   if (!all_aligned(d_src, n) || !aligned16(d_dst)) return ECW_EALIGN;
@@ -654,8 +707,8 @@ int ecw_encode_batch_split_dev(ecw_codec* c, const uint8_t* d_data, size_t data_
   if (!aligned16(d_data) || !aligned16(d_parity) || data_block_stride % 16 || data_stripe_stride % 16 ||
       parity_block_stride % 16 || parity_stripe_stride % 16)
     return ECW_EALIGN;
-  if (stripes > 1 && (data_stripe_stride < (k - 1) * data_block_stride + len ||
-                      parity_stripe_stride < (np - 1) * parity_block_stride + len))
+  if (!disjoint_units(data_block_stride, data_stripe_stride, k, stripes, len) ||
+      !disjoint_units(parity_block_stride, parity_stripe_stride, np, stripes, len))
     return ECW_EINVAL;
   {
     std::lock_guard<std::mutex> lk(c->mu);

@@ -43,6 +43,15 @@ inline SlabRows slab_rows(const uint8_t* base, uint64_t bstride, uint64_t sstrid
                   bstride, sstride};
 }
 
+// Pointer tables in device memory for a batch of stripes (ecw_encode_ptrs_dev):
+// data block j of stripe s at src[s*k + j], output o of stripe s at
+// dst[s*np + o] (o in [G_0..G_{m-1}, L_0..L_{g-1}] order).
+struct PtrTabRows {
+  const uint8_t* const* src;
+  uint8_t* const* dst;
+  int np;
+};
+
 struct EncodeGeom {
   uint64_t len;          // bytes per block
   uint64_t tiles;        // column tiles per stripe = ceil(len / kTileBytes)
@@ -75,6 +84,8 @@ hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const voi
                              hipStream_t s, TicketCounter* tc);
 hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl,
                               hipStream_t s, TicketCounter* tc);
+hipError_t launch_encode_tab(const PtrTabRows& rows, const EncodeGeom& g, const void* d_tbl,
+                             hipStream_t s, TicketCounter* tc);
 // true when an encode of `tiles` column tiles at k data rows would use a ticket counter
 bool encode_uses_ticket(uint64_t tiles, int k);
 

@@ -138,6 +138,15 @@ __device__ __forceinline__ const uint8_t* src_row(const PtrRows& r, const Encode
 __device__ __forceinline__ const uint8_t* src_row(const SlabRows& r, const EncodeGeom&, int s, int j) {
   return r.base + s * r.sstride + static_cast<uint64_t>(j) * r.bstride;
 }
+__device__ __forceinline__ const uint8_t* src_row(const PtrTabRows& r, const EncodeGeom& g, int s, int j) {
+  return r.src[static_cast<uint64_t>(s) * g.k + j];
+}
+__device__ __forceinline__ uint8_t* glob_row(const PtrTabRows& r, const EncodeGeom& g, int s, int l) {
+  return r.dst[static_cast<uint64_t>(s) * r.np + g.row0 + l];
+}
+__device__ __forceinline__ uint8_t* local_row(const PtrTabRows& r, const EncodeGeom& g, int s, int t) {
+  return r.dst[static_cast<uint64_t>(s) * r.np + g.m + t];
+}
 __device__ __forceinline__ uint8_t* glob_row(const PtrRows& r, const EncodeGeom&, int, int l) {
   return r.dst[l];
 }
@@ -408,6 +417,14 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
         encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * pbs),
                                                 const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * pbs), bs,
                                                 pbs, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+      } else if constexpr (std::is_same<Rows, PtrTabRows>::value) {
+        // this stripe's rows of the device pointer tables, read with s_load
+        const uint64_t s = static_cast<uint64_t>(cur.s);
+        const uint8_t* st = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.src + s * k));
+        const uint8_t* dt = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.dst + s * rows.np));
+        encode_tile_asm<LOCAL, PARK, true, NW>(st, const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.m) * sizeof(void*)),
+                                           const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.row0) * sizeof(void*)),
+                                           0, 0, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
       } else {
         const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
             reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
@@ -726,6 +743,10 @@ hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const voi
 hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
                               TicketCounter* tc) {
   return launch_encode(slab, g, d_tbl, s, tc);
+}
+hipError_t launch_encode_tab(const PtrTabRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
+                             TicketCounter* tc) {
+  return launch_encode(rows, g, d_tbl, s, tc);
 }
 bool encode_uses_ticket(uint64_t tiles, int k) {
   return ECW_ENC_ASM && k >= 2 && ECW_TICKET_MIN_TILES > 0 && tiles >= ECW_TICKET_MIN_TILES;

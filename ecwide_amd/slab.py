@@ -1,13 +1,19 @@
 """Batches of independent stripes resident in HBM (the north_star layout).
 
 A ``StripeSlab`` is one torch uint8 CUDA allocation holding ``stripes``
-stripes. Two layouts:
+stripes. Three layouts:
 
 * ``"blocks"`` (default): stripe s starts at ``s * stripe_stride`` and block b
   of a stripe at ``b * block_stride``, blocks ordered [D_0..D_{k-1},
   G_0..G_{m-1}, L_0..L_{g-1}] (the D/G/L order ChunkGenerator.java:51-103
   writes). The block stride is padded past B (default +4 KiB) so the k
   concurrent row streams of a stripe do not all start on the same HBM channel.
+* ``"split"``: whole contiguous blocks as in "blocks", but the data blocks of
+  all stripes form one region and the parity blocks of all stripes a second
+  one after it (ecw_encode_batch_split_dev). Parity rows interleaved with the
+  data rows at one stride (the "blocks" slab) cost the encode ~10 %; in a
+  region of their own the block layout encodes at the tiled slab's rate
+  (tools/rw_layout.py).
 * ``"tiled"``: every block is cut into ``chunk``-byte column pieces; piece c
   of the k data blocks of stripe s is one contiguous run of k * chunk bytes
   (data region), piece c of the m + g parities one run in the parity region
@@ -51,6 +57,12 @@ class StripeSlab:
             self.block_stride = (self.len + pad + 255) // 256 * 256
             self.stripe_stride = self.nblocks * self.block_stride
             nbytes = stripes * self.stripe_stride
+        elif layout == "split":
+            self.block_stride = (self.len + pad + 255) // 256 * 256
+            self.stripe_stride = k * self.block_stride      # data region
+            self.pstripe_stride = np_ * self.block_stride   # parity region
+            self.parity_offset = stripes * self.stripe_stride
+            nbytes = self.parity_offset + stripes * self.pstripe_stride
         elif layout == "tiled":
             if chunk % 256 or chunk <= 0 or self.len % chunk:
                 raise ValueError("tiled layout: chunk must be a positive multiple of 256 dividing the block size")
@@ -69,6 +81,10 @@ class StripeSlab:
         self.base = self.buf.data_ptr()
 
     def _split_args(self):
+        if self.layout == "split":
+            bs = self.block_stride
+            return (c_void_p(self.base), bs, self.stripe_stride, c_void_p(self.base + self.parity_offset), bs,
+                    self.pstripe_stride)
         ch = self.chunk
         return (c_void_p(self.base), ch, self.unit_stride, c_void_p(self.base + self.parity_offset), ch,
                 self.punit_stride)
@@ -79,7 +95,12 @@ class StripeSlab:
         if self.layout == "blocks":
             o = s * self.stripe_stride + b * self.block_stride
             return self.buf[o:o + self.len]
-        k, np_, ch = self.codec.encodeDataNum, self.codec.parityNum, self.chunk
+        k, np_ = self.codec.encodeDataNum, self.codec.parityNum
+        if self.layout == "split":
+            o = (s * self.stripe_stride + b * self.block_stride if b < k else
+                 self.parity_offset + s * self.pstripe_stride + (b - k) * self.block_stride)
+            return self.buf[o:o + self.len]
+        ch = self.chunk
         if b < k:
             o, step = s * self.pieces * self.unit_stride + b * ch, self.unit_stride
         else:
@@ -104,7 +125,7 @@ class StripeSlab:
         if self.layout == "tiled":
             ch = self.chunk
             args = (ch, self.pieces * self.unit_stride, self.stripes, k, self.len, ch, self.unit_stride)
-        else:
+        else:  # blocks / split: the data blocks at block_stride, stripes at stripe_stride
             args = (self.block_stride, self.stripe_stride, self.stripes, k, self.len, max(16, self.out_stride), 0)
         _check(lib.ecw_fill_random_pieces_dev(self.codec.device, c_void_p(self.base), *args, col_offset, seed, s0, 0,
                                               _stream()), "fill_random")
@@ -113,6 +134,10 @@ class StripeSlab:
         st = stream if stream is not None else _stream()
         if self.layout == "tiled":
             _check(lib.ecw_encode_batch_split_dev(self.codec._h, *self._split_args(), self.units, self.chunk, st),
+                   "encode_batch_split")
+            return
+        if self.layout == "split":
+            _check(lib.ecw_encode_batch_split_dev(self.codec._h, *self._split_args(), self.stripes, self.len, st),
                    "encode_batch_split")
             return
         _check(lib.ecw_encode_batch_dev(self.codec._h, c_void_p(self.base), self.block_stride,
@@ -127,6 +152,11 @@ class StripeSlab:
                 raise ValueError("tiled layout: repair outputs are contiguous blocks (out_stride = block size)")
             _check(lib.ecw_repair_batch_split_dev(self.codec._h, *self._split_args(), self.units, lost_block,
                                                   c_void_p(out.data_ptr()), self.chunk, self.chunk,
+                                                  stream if stream is not None else _stream()), "repair_split")
+            return
+        if self.layout == "split":
+            _check(lib.ecw_repair_batch_split_dev(self.codec._h, *self._split_args(), self.stripes, lost_block,
+                                                  c_void_p(out.data_ptr()), ostride, self.len,
                                                   stream if stream is not None else _stream()), "repair_split")
             return
         _check(lib.ecw_repair_batch_dev(self.codec._h, c_void_p(self.base), self.block_stride,

@@ -204,6 +204,16 @@ int ecw_partial_decode_dev(ecw_codec* codec, const uint8_t* const* d_data, uint8
                            size_t len, void* stream);
 int ecw_xor_intermediate_dev(ecw_codec* codec, const uint8_t* const* d_source,
                              uint8_t* const* d_target, size_t len, void* stream);
+/* Encode `stripes` stripes of separately placed HBM blocks in ONE launch (the
+ * reference's per-block pointer convention, NativeCodec.cc:158-166, batched):
+ * d_data_ptrs and d_parity_ptrs are DEVICE arrays (8-byte aligned) of
+ * stripes*k data block pointers (stripe-major) and stripes*parity_num output
+ * pointers ([G_0..G_{m-1}, L_0..L_{g-1}] per stripe). Every block is `len`
+ * bytes, 16-byte aligned (the caller's guarantee: the pointers are not read
+ * on the host). Codecs with local groups but no global row (m = 0) are
+ * ECW_EUNSUPPORTED here. */
+int ecw_encode_ptrs_dev(ecw_codec* codec, int stripes, const uint8_t* const* d_data_ptrs,
+                        uint8_t* const* d_parity_ptrs, size_t len, void* stream);
 /* target = XOR of n device blocks (the arithmetic of decode / partial decode
  * / relayer stage for any fan-in); n in [1, 256]. */
 int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* d_dst, size_t len,
@@ -223,7 +233,11 @@ int ecw_encode_batch_dev(ecw_codec* codec, uint8_t* d_slab, size_t block_stride,
  * strided batches): data block j of stripe s at
  * d_data + s*data_stripe_stride + j*data_block_stride, parity block i
  * ([G_0..G_{m-1}, L_0..L_{g-1}]) at d_parity + s*parity_stripe_stride +
- * i*parity_block_stride. The regions must not overlap. With 4 KiB "stripes"
+ * i*parity_block_stride. The regions must not overlap. Within a region the
+ * stripes follow one another (stripe stride >= the stripe's extent) or are
+ * interleaved inside every block (stripe stride >= len and block stride >=
+ * (stripes-1)*stripe stride + len: e.g. the column pieces of one stripe of
+ * whole blocks, each encoded as a stripe of its own). With 4 KiB "stripes"
  * (block stride 4096, stripe stride k*4096) it encodes a tiled layout in
  * which every 4 KiB column of the k data blocks is contiguous. */
 int ecw_encode_batch_split_dev(ecw_codec* codec, const uint8_t* d_data, size_t data_block_stride,

@@ -220,7 +220,7 @@ def test_xor_every_source_count(E, torch, orc):
         assert np.array_equal(out.cpu().numpy(), orc.xor_blocks(data)), n
 
 
-@pytest.mark.parametrize("layout", ["blocks", "tiled"])
+@pytest.mark.parametrize("layout", ["blocks", "split", "tiled"])
 @pytest.mark.parametrize("k,r", [(40, 40), (64, 31), (64, 32), (70, 33), (12, 1)])
 def test_repair_group_sizes(E, torch, k, r, layout):
     """CL repair of D0, the group's last block and L0 with r + 1 survivors on
@@ -357,6 +357,65 @@ def test_hbm_filling_batch_configs3(E, torch, orc):
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("k,m,r,B,S,local", [
+    (128, 3, 27, 1 << 16, 3, "xor"),             # the bench shape, u32-entry asm tile, parked locals
+    (20, 6, 4, 3 * 4096 + 48, 2, "xor"),         # 5-8 rows (u64 tile), 5 groups, ragged tail
+    (30, 11, 4, 8192, 2, "literal"),             # two passes (8 + 3 rows), 8 groups not parked, zero L
+    (1, 2, 1, 5000, 3, "xor"),                   # k = 1: the C++ tile
+    (33, 3, 4, 4096 * 3, 4, "xor"),              # odd k, > 5 groups
+])
+def test_encode_ptrs_dev_vs_oracle(E, torch, orc, k, m, r, B, S, local):
+    """ecw_encode_ptrs_dev: a batch of stripes whose blocks are separate
+    allocations, one launch, pointers in device tables (BlockBatch /
+    NativeCodec.encodeStripes) vs the oracle."""
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
+    oc = orc.codec("C", k, m, r, B)
+    data = [[torch.from_numpy(orc.fill(B, 500 + s, s, j)).cuda() for j in range(k)] for s in range(S)]
+    par = [[torch.full((B + 32,), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(c.parityNum)]
+           for _ in range(S)]
+    c.encodeStripes(data, [[p[:B] for p in ps] for ps in par])
+    torch.cuda.synchronize()
+    for s in range(S):
+        want = oc.encode([d.cpu().numpy() for d in data[s]], literal=local == "literal", threads=8)
+        for i, w in enumerate(want):
+            got = par[s][i].cpu().numpy()
+            assert np.array_equal(got[:B], w), (s, i)
+            assert (got[B:] == 0x5A).all(), ("wrote past the block", s, i)
+
+
+def test_encode_ptrs_dev_ticket_and_errors(E, torch, orc):
+    """>= 262,144 tiles through the pointer tables take the ticket-ordered
+    launch (twice on one stream: the counter carries over); the result equals
+    the split slab's encode of the same bytes. Misaligned tables and m = 0
+    are refused."""
+    from ctypes import c_void_p
+
+    from ecwide_amd._lib import lib
+
+    k, m, r, B, S = 4, 2, 2, 256 << 20, 4
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout="split")
+    slab.fill_random(seed=8)
+    slab.encode()
+    par = [[torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(c.parityNum)] for _ in range(S)]
+    batch = E.BlockBatch(c, [slab.data(s) for s in range(S)], par)
+    batch.encode()
+    batch.encode()
+    torch.cuda.synchronize()
+    for s in range(S):
+        for i, p in enumerate(slab.parity(s)):
+            assert torch.equal(p, par[s][i]), (s, i)
+    st = lib.ecw_encode_ptrs_dev(c._h, S, c_void_p(batch.dtab.data_ptr() + 4), c_void_p(batch.ptab.data_ptr()), B,
+                                 c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == -4
+    c0 = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(8, 0, 4, 4096), 1, False)
+    st = lib.ecw_encode_ptrs_dev(c0._h, 1, c_void_p(batch.dtab.data_ptr()), c_void_p(batch.ptab.data_ptr()), 4096,
+                                 c_void_p(torch.cuda.current_stream().cuda_stream))
+    assert st == -5
+    del slab, batch, par
+    torch.cuda.empty_cache()
+
+
 def test_decode_partial_xor_golden(E, torch, orc, manifest):
     for e in manifest["xor_reduce"]:
         data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["n"])]
@@ -458,11 +517,13 @@ def test_fill_same_bytes_in_every_layout(E, torch, orc, chunk, col_offset):
                                        # the 5-8-row asm tile: parked (<= 5 groups) and not, k = 2 / 3
                                        (128, 6, 27, 1 << 16, 2), (40, 8, 7, 3 * 4096 + 48, 2),
                                        (3, 7, 2, 8192, 2), (2, 5, 1, 4096, 2)])
-def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S):
-    """Batched slab encode vs oracle at mid sizes; repair of every data and
-    local block of stripe 0 equals the erased block."""
+@pytest.mark.parametrize("layout", ["blocks", "split"])
+def test_slab_encode_repair_vs_oracle(E, torch, orc, k, m, r, B, S, layout):
+    """Batched slab encode vs oracle at mid sizes, in-slab parities (ChunkGenerator
+    order) and the split slab; repair of every data and local block equals
+    the erased block."""
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
-    slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout=layout)
     slab.fill_random(seed=99)
     slab.encode()
     torch.cuda.synchronize()
