@@ -84,6 +84,10 @@ def parse(argv=None):
                     help="with --host-resident: ordinary pageable host blocks instead of pinned ones")
     ap.add_argument("--host-resident", action="store_true",
                     help="measure the PCIe-inclusive rate (pinned host blocks) instead")
+    ap.add_argument("--small-calls", action="store_true",
+                    help="measure ECWide-H's synchronous one-chunk ec_encode_data calls (k=11, m=3) instead")
+    ap.add_argument("--small-len", type=int, default=4096)
+    ap.add_argument("--small-calls-n", type=int, default=5000, help="calls per thread")
     return ap.parse_args(argv)
 
 
@@ -425,6 +429,86 @@ def host_resident(args):
     print(json.dumps(line), flush=True)
 
 
+# ---- ECWide-H's synchronous small calls ----------------------------------------
+def small_calls(args):
+    """ECWide-H encodes one chunk per synchronous ISA-L call (g_encode:
+    ec_encode_data(4096, GK=11, 3, ...), ECWide-H/proxy/encode.cpp:145-175),
+    from its proxy threads (proxy.cpp:2001-2012). Here the same calls go
+    through libecw_isal.so (the ISA-L-signature shim) to the GPU's resident
+    request service; the CPU baseline is the oracle's AVX2 port of ISA-L's
+    kernel making the same calls from one thread. Both sides are driven from
+    Python through ctypes (same per-call overhead on both)."""
+    import ctypes
+    import threading
+
+    import numpy as np
+
+    import ecwide_amd  # noqa: F401  (torch first, then libecwide.so)
+
+    k, m, ln = 11, 3, args.small_len
+    shim = ctypes.CDLL(os.path.join(REPO, "ecwide_amd", "libecw_isal.so"))
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    full = np.zeros((k + m) * k, np.uint8)
+    shim.gf_gen_cauchy1_matrix(full.ctypes.data_as(u8p), k + m, k)
+    tbl = np.zeros(32 * k * m, np.uint8)
+    shim.ec_init_tables(k, m, full[k * k:].copy().ctypes.data_as(u8p), tbl.ctypes.data_as(u8p))
+    tp = tbl.ctypes.data_as(u8p)
+    rng = np.random.default_rng(args.seed)
+
+    def buffers():
+        d = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k)]
+        p = [np.zeros(ln, np.uint8) for _ in range(m)]
+        return d, p, (u8p * k)(*[x.ctypes.data_as(u8p) for x in d]), (u8p * m)(*[x.ctypes.data_as(u8p) for x in p])
+
+    # parity of the first call vs the oracle (outside the timing)
+    import oracle
+
+    orc = oracle.Oracle()
+    d0, p0, dp0, pp0 = buffers()
+    shim.ec_encode_data(ln, k, m, tp, dp0, pp0)
+    want = orc.encode_data(tbl, d0, m, avx2=True)
+    verified = all(np.array_equal(a, b) for a, b in zip(p0, want))
+
+    def run_threads(nt, calls, fn):
+        bufs = [buffers() for _ in range(nt)]
+        for b in bufs:
+            fn(b)  # warm
+        def work(b):
+            for _ in range(calls):
+                fn(b)
+        th = [threading.Thread(target=work, args=(b,)) for b in bufs]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        n = nt * calls
+        return {"threads": nt, "calls": n, "us_per_call_per_thread": round(el / calls * 1e6, 2),
+                "calls_per_s": round(n / el), "GBps": round(n * (k + m) * ln / el / 1e9, 3)}
+
+    gpu = [run_threads(nt, args.small_calls_n, lambda b: shim.ec_encode_data(ln, k, m, tp, b[2], b[3]))
+           for nt in (1, 4, 16)]
+    L = orc.L
+
+    def cpu_call(b):
+        L.orc_encode_data_avx2(ln, k, m, tp, b[2], b[3])
+
+    cpu = run_threads(1, max(args.small_calls_n, 20000), cpu_call)
+    line = {
+        "metric": "synchronous small encode calls GB/s (ECWide-H g_encode: ec_encode_data one 4 KiB chunk per call)",
+        "value": gpu[0]["GBps"], "unit": "GB/s", "n_gpus": 1, "higher_is_better": True,
+        "config": {"workload": f"RS-Cauchy k={k}, m={m}, {ln} B blocks, one stripe per synchronous call from each "
+                               f"thread, through libecw_isal.so (ISA-L signatures) to the resident request service",
+                   "bytes_per_call": (k + m) * ln},
+        "threads": gpu, "verified": bool(verified),
+        "cpu_baseline": dict(cpu, value=cpu["GBps"], unit="GB/s", cores=1, kind="port",
+                             sample="the same calls on the oracle's AVX2 port of ISA-L gf_3vect_dot_prod_avx2, "
+                                    "1 thread", host_cpu=host_cpu_model()),
+    }
+    print(json.dumps(line), flush=True)
+
+
 # ---- the bench ------------------------------------------------------------------
 def dry_run(args, d: Dist):
     """The N>1 orchestration without a GPU: plans, a stand-in timed region
@@ -458,6 +542,9 @@ def main():
         sys.exit(spawn_ranks(args.gpus, argv))
     if args.host_resident:
         host_resident(args)
+        return
+    if args.small_calls:
+        small_calls(args)
         return
     d = Dist(args)
     if args.dry_run:

@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cctype>
+#include <chrono>
+#include <condition_variable>
 #include <cerrno>
 #include <climits>
 #include <cstdio>
@@ -956,9 +958,217 @@ static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout
   return run_xor_ptr(din, nin, dout[0], len, s);
 }
 
+// ---- small-stripe request service (ecw_internal.hpp SvcCtl) -----------------
+// One synchronous small encode = copy the blocks into a slot's pinned staging,
+// bump the slot's `seq`, spin on `done`, copy the parities out: no launch, no
+// stream synchronisation, no DMA setup. The resident kernel is (re)launched on
+// demand and leaves by itself after ECW_SERVICE_IDLE_MS (default 20) ms with no
+// request on any slot. ECW_SERVICE=0 turns the service off.
+namespace svc {
+
+constexpr int kNotServed = 1;  // not an error: the caller takes the launch path
+
+bool enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("ECW_SERVICE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
+struct Service {
+  int device = -1;
+  std::mutex mu;  // everything below
+  std::condition_variable cv;
+  bool broken = false;
+  SvcCtl* ctl = nullptr;    // coherent pinned host memory (host view)
+  SvcCtl* d_ctl = nullptr;  // its device view
+  SvcDev* d_state = nullptr;
+  hipStream_t stream = nullptr;
+  unsigned long long epoch = 0;  // last epoch launched (0: none yet)
+  unsigned long long idle_ticks = 0, life_ticks = 0;
+  std::vector<int> free_slots;
+  uint8_t* stage[kSvcSlots] = {};
+  uint8_t* d_stage[kSvcSlots] = {};
+  size_t stage_bytes[kSvcSlots] = {};
+
+  int init() {
+    DeviceGuard g(device);
+    if (!g.ok) return ECW_EDEVICE;
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) != hipSuccess || khz <= 0)
+      return ECW_EDEVICE;
+    const char* e = std::getenv("ECW_SERVICE_IDLE_MS");
+    const unsigned long long idle_ms = e ? std::strtoull(e, nullptr, 10) : 20;
+    idle_ticks = idle_ms * static_cast<unsigned long long>(khz);
+    life_ticks = 2000ull * static_cast<unsigned long long>(khz);
+    void* h = nullptr;
+    if (hipHostMalloc(&h, sizeof(SvcCtl), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
+      return ECW_ENOMEM;
+    std::memset(h, 0, sizeof(SvcCtl));
+    void* dv = nullptr;
+    if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess || hipMalloc(&d_state, sizeof(SvcDev)) != hipSuccess ||
+        hipStreamCreateWithFlags(&stream, hipStreamNonBlocking) != hipSuccess) {
+      (void)hipHostFree(h);
+      if (d_state) (void)hipFree(d_state);
+      d_state = nullptr;
+      return ECW_EDEVICE;
+    }
+    ctl = static_cast<SvcCtl*>(h);
+    d_ctl = static_cast<SvcCtl*>(dv);
+    for (int i = kSvcSlots - 1; i >= 0; --i) free_slots.push_back(i);
+    return ECW_OK;
+  }
+
+  // launch the next epoch unless the current one is still serving (under mu)
+  int ensure_running() {
+    if (epoch != 0 && __atomic_load_n(&ctl->exited_epoch, __ATOMIC_ACQUIRE) != epoch) return ECW_OK;
+    DeviceGuard g(device);
+    if (!g.ok || hipMemsetAsync(d_state, 0, sizeof(SvcDev), stream) != hipSuccess) return ECW_EDEVICE;
+    if (launch_service(d_ctl, d_state, epoch + 1, idle_ticks, life_ticks, stream) != hipSuccess) return ECW_EDEVICE;
+    ++epoch;
+    return ECW_OK;
+  }
+
+  int ensure_stage(int slot, size_t bytes) {
+    if (stage_bytes[slot] >= bytes) return ECW_OK;
+    if (stage[slot]) (void)hipHostFree(stage[slot]);
+    stage[slot] = d_stage[slot] = nullptr;
+    stage_bytes[slot] = 0;
+    void* h = nullptr;
+    void* dv = nullptr;
+    if (hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return ECW_ENOMEM;
+    if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess) {
+      (void)hipHostFree(h);
+      return ECW_EDEVICE;
+    }
+    stage[slot] = static_cast<uint8_t*>(h);
+    d_stage[slot] = static_cast<uint8_t*>(dv);
+    stage_bytes[slot] = bytes;
+    return ECW_OK;
+  }
+
+  void stop() {
+    std::lock_guard<std::mutex> lk(mu);
+    if (!ctl || epoch == 0) return;
+    __atomic_store_n(&ctl->stop, 1ull, __ATOMIC_RELEASE);
+    DeviceGuard g(device);
+    (void)hipStreamSynchronize(stream);
+    __atomic_store_n(&ctl->stop, 0ull, __ATOMIC_RELEASE);
+  }
+};
+
+std::mutex g_mu;
+std::map<int, Service*> g_services;  // one per device, kept for the life of the process
+
+void stop_all() {
+  std::lock_guard<std::mutex> lk(g_mu);
+  for (auto& kv : g_services) kv.second->stop();
+}
+
+Service* service_for(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  Service*& sv = g_services[device];
+  if (!sv) {
+    if (g_services.size() == 1) std::atexit(stop_all);  // leave every resident kernel before the runtime goes
+    sv = new Service();
+    sv->device = device;
+  }
+  return sv;
+}
+
+// Serve one stripe, or return kNotServed (shape or state not suitable).
+int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
+  const int k = c->k(), m = c->m(), np = c->info.parity_num;
+  const int nw = m <= 4 ? 1 : 2;
+  if (!enabled() || m < 1 || m > kMaxPassRows || len == 0 || len > kSvcMaxLen ||
+      static_cast<size_t>(k) * 128 * nw > kSvcLds)
+    return kNotServed;
+  {
+    std::lock_guard<std::mutex> lk(c->mu);
+    if (c->ensure_device() != ECW_OK) return kNotServed;  // the launch path reports the error
+  }
+  Service* sv = service_for(c->device);
+  const size_t cs = (len + 255) & ~static_cast<size_t>(255);
+  int slot;
+  {
+    std::unique_lock<std::mutex> lk(sv->mu);
+    if (sv->broken) return kNotServed;
+    if (!sv->ctl && sv->init() != ECW_OK) {
+      sv->broken = true;
+      return kNotServed;
+    }
+    sv->cv.wait(lk, [&] { return !sv->free_slots.empty(); });
+    slot = sv->free_slots.back();
+    sv->free_slots.pop_back();
+    if (sv->ensure_stage(slot, cs * (k + np)) != ECW_OK) {
+      sv->free_slots.push_back(slot);
+      sv->cv.notify_one();
+      return kNotServed;
+    }
+  }
+  auto release = [&](int st) {
+    std::lock_guard<std::mutex> lk(sv->mu);
+    sv->free_slots.push_back(slot);
+    sv->cv.notify_one();
+    return st;
+  };
+  uint8_t* h = sv->stage[slot];
+  for (int j = 0; j < k; ++j) std::memcpy(h + j * cs, data[j], len);
+  SvcSlot& q = sv->ctl->slot[slot];
+  q.tbl = c->d_pass[0];
+  q.data = sv->d_stage[slot];
+  q.out = sv->d_stage[slot] + static_cast<size_t>(k) * cs;
+  q.len = len;
+  q.cs = cs;
+  q.k = k;
+  q.nrows = m;
+  q.m = m;
+  q.r = c->has_local() ? c->r() : k;
+  q.groups = c->groups();
+  q.local_mode = local_mode_of(c);
+  q.nw = nw;
+  const unsigned long long seq = q.seq + 1;  // only this thread writes the slot while it holds it
+  __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
+  {
+    std::lock_guard<std::mutex> lk(sv->mu);
+    if (sv->ensure_running() != ECW_OK) {
+      sv->broken = true;
+      return release(ECW_EDEVICE);
+    }
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (unsigned spins = 1; __atomic_load_n(&q.done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+    if (spins % 1024) {
+      __builtin_ia32_pause();
+      continue;
+    }
+    std::lock_guard<std::mutex> lk(sv->mu);
+    if (__atomic_load_n(&q.done, __ATOMIC_ACQUIRE) == seq) break;
+    // the epoch this request was posted to left before serving it: start the next one
+    if (sv->ensure_running() != ECW_OK) {
+      sv->broken = true;
+      return release(ECW_EDEVICE);
+    }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      sv->broken = true;  // a request that takes 10 s means the device is gone: stop using the service
+      return release(ECW_EDEVICE);
+    }
+  }
+  for (int i = 0; i < np; ++i) std::memcpy(parity[i], h + static_cast<size_t>(k + i) * cs, len);
+  return release(ECW_OK);
+}
+
+}  // namespace svc
+
 int ecw_encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
   if (!c || !data || !parity || !check_len(len)) return ECW_EINVAL;
-  // small blocks: one packed stripe (two copy calls instead of one per block)
+  for (int j = 0; j < c->k(); ++j)
+    if (!data[j]) return ECW_EINVAL;
+  for (int i = 0; i < c->info.parity_num; ++i)
+    if (!parity[i]) return ECW_EINVAL;
+  // small blocks: the resident request service, else one packed stripe (two
+  // copy calls instead of one per block)
   if (len > 0 && len <= kSmallBlock) return ecw_encode_stripes(c, 1, data, parity, len);
   return host_roundtrip(c, data, c->k(), parity, c->info.parity_num, len, op_encode);
 }
@@ -1091,6 +1301,10 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
   for (size_t i = 0; i < static_cast<size_t>(stripes) * np; ++i)
     if (!parity[i]) return ECW_EINVAL;
   if (len == 0 || stripes == 0) return ECW_OK;
+  if (stripes == 1 && len <= kSvcMaxLen) {
+    const int sst = svc::encode(c, data, parity, len);
+    if (sst != svc::kNotServed) return sst;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   int st = c->ensure_device();
   if (st) return st;

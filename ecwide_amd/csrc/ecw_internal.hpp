@@ -126,4 +126,47 @@ hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, 
 
 int device_cu_count(int device);
 
+// ---- small-stripe request service (ecw_codec.cpp: svc::) -------------------
+// A resident kernel serves synchronous small encodes (ECWide-H encodes one
+// 4 KiB chunk per ec_encode_data call, ECWide-H/proxy/encode.cpp:145-175)
+// without a launch or a stream synchronisation per call: workgroup i polls
+// slot i of a control block in coherent pinned host memory, reads the
+// request's blocks from pinned staging over PCIe, writes the parities back
+// there and publishes `done`. Every workgroup leaves the loop on the stop flag,
+// once NO slot has had a request for `idle_ticks` of wall clock, or after
+// `life_ticks`; the last one out publishes exited_epoch = epoch, and the host
+// launches the next epoch when a request finds the service gone.
+constexpr int kSvcSlots = 16;  // concurrent callers served at once (one workgroup each)
+constexpr size_t kSvcMaxLen = size_t(64) << 10;   // bytes per block served (larger: launch path)
+constexpr size_t kSvcLds = size_t(60) << 10;       // LDS for the packed tables: k * 128 * nw bytes
+
+struct alignas(64) SvcSlot {
+  unsigned long long seq;    // host: number of the latest request
+  unsigned long long pad0[7];
+  unsigned long long done;   // device: number of the latest finished request
+  unsigned long long pad1[7];
+  // the request (written by the host before `seq`)
+  const void* tbl;           // packed tables of the codec's pass 0 (device memory)
+  uint8_t* data;             // k input rows, `cs` bytes apart (device view of pinned staging)
+  uint8_t* out;              // parity rows [G.., L..], `cs` bytes apart
+  unsigned long long len, cs;
+  int k, nrows, m, r, groups, local_mode, nw, pad2;
+};
+
+struct SvcCtl {
+  unsigned long long stop;          // host: leave now
+  unsigned long long exited_epoch;  // device: the epoch that last left the loop
+  unsigned long long pad[6];
+  SvcSlot slot[kSvcSlots];
+};
+
+// device-memory state of one service launch (zeroed before every launch)
+struct SvcDev {
+  unsigned long long last_active;  // wall clock of the latest request served by any workgroup
+  unsigned int exited;             // workgroups that left the loop
+};
+
+hipError_t launch_service(SvcCtl* d_ctl, SvcDev* d_state, unsigned long long epoch, unsigned long long idle_ticks,
+                          unsigned long long life_ticks, hipStream_t s);
+
 }  // namespace ecw

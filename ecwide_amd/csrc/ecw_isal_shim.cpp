@@ -12,14 +12,17 @@
 // isal:erasure_code/ec_base.c:290-305) and runs a cached matrix codec
 // (ecw_matrix_codec_create) through the host-memory pipeline.
 //
-// Concurrent callers are batched (group commit): ECWide-H calls
-// ec_encode_data on 4 KiB chunks from four proxy threads
-// (ECWide-H/proxy/proxy.cpp:2001-2012), and one GPU round trip costs far more
-// than 4 KiB of work. A call joins the pending list of its (codec, len); if
-// no batch of that key is running, the caller runs everything pending as one
-// ecw_encode_stripes call (one launch, packed copies); otherwise it waits and
-// is picked up by the next batch. A lone caller runs at once -- there is no
-// timer. ECW_ISAL_BATCH=0 turns batching off (one ecw_encode per call).
+// ECWide-H calls ec_encode_data on 4 KiB chunks from four proxy threads
+// (ECWide-H/proxy/proxy.cpp:2001-2012). Each call is one synchronous request
+// to libecwide's resident request service (ecw_encode -> svc::encode), which
+// serves concurrent callers on separate slots. With the service off
+// (ECW_SERVICE=0) one GPU round trip costs far more than 4 KiB of work, so
+// concurrent callers are batched instead (group commit): a call joins the
+// pending list of its (codec, len); if no batch of that key is running, the
+// caller runs everything pending as one ecw_encode_stripes call (one launch,
+// packed copies); otherwise it waits and is picked up by the next batch. A
+// lone caller runs at once -- there is no timer. ECW_ISAL_BATCH=1/0 forces
+// batching on/off.
 //
 // The ISA-L functions return void; a failure is reported on stderr and by
 // ecw_isal_last_status() (per thread), never by exit().
@@ -91,10 +94,16 @@ ecw_codec* codec_for(int k, int rows, const unsigned char* gftbls) {
   return cd;
 }
 
+// Group commit pays off only without the resident request service: the
+// service gives each concurrent caller a slot of its own (15 us per 4 KiB call
+// from 4 threads at once, against 70 us when batched into launches; DESIGN.md
+// section 8). ECW_ISAL_BATCH=1 / 0 forces it on / off.
 bool batching_on() {
   static const bool on = [] {
     const char* e = std::getenv("ECW_ISAL_BATCH");
-    return !(e && e[0] == '0');
+    if (e) return e[0] != '0';
+    const char* s = std::getenv("ECW_SERVICE");
+    return s && s[0] == '0';
   }();
   return on;
 }

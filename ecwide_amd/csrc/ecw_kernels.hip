@@ -734,7 +734,178 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---- small-stripe request service (ecw_internal.hpp SvcCtl) ----------------
+__device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ unsigned long long sys_load_relaxed(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void sys_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// The request as the workgroup sees it (copied from the slot by lane 0).
+struct SvcReq {
+  const uint4* tbl;
+  uint8_t* data;
+  uint8_t* out;
+  unsigned long long len, cs;
+  int k, nrows, m, r, groups, local_mode, nw, pad;
+};
+constexpr int kSvcReqWords = 9;
+static_assert(sizeof(SvcReq) == 8 * kSvcReqWords, "SvcReq mirrors the request words of SvcSlot");
+static_assert(offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl) == sizeof(SvcReq), "SvcSlot request layout");
+
+// One lane's 16 columns of a served request. All input rows of a round of 16
+// are loaded before the first product: they come from pinned host memory, so
+// one PCIe round trip per 16 rows, not one per ring slot. Full lanes load every
+// row of the round unconditionally (rows past k re-read row k-1) with the
+// volatile buffer load, so the compiler keeps all 16 loads in flight.
+template <int NW, int LOCAL, bool TAIL>
+__device__ __forceinline__ void svc_columns(const SvcReq& q, uint32_t lds_base, uint32_t col) {
+  const uint32_t len = static_cast<uint32_t>(q.len);
+  const int k = q.k;
+  uint32_t acc[16 * NW];
+#pragma unroll
+  for (int i = 0; i < 16 * NW; ++i) acc[i] = 0;
+  uint4 lacc = make_uint4(0, 0, 0, 0);
+  int gend = q.r < k ? q.r : k, t = 0;
+  for (int j0 = 0; j0 < k; j0 += 16) {
+    uint4 v[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const uint8_t* row = q.data + static_cast<uint64_t>(j0 + u < k ? j0 + u : k - 1) * q.cs;
+      v[u] = ld16<TAIL>(uniform_ptr(row), col, len);
+    }
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = j0 + u;
+      if (j >= k) continue;
+      gf_row<NW>(v[u], acc, lds_base + static_cast<uint32_t>(j) * (128u * NW));
+      if constexpr (LOCAL != kLocalNone) {
+        lacc = xor4(lacc, v[u]);
+        if (j + 1 == gend) {
+          st16<true>(q.out + static_cast<uint64_t>(q.m + t) * q.cs, col, len,
+                     LOCAL == kLocalXor ? lacc : make_uint4(0, 0, 0, 0));
+          lacc = make_uint4(0, 0, 0, 0);
+          ++t;
+          gend = gend + q.r < k ? gend + q.r : k;
+        }
+      }
+    }
+  }
+  for (int l = 0; l < q.nrows; ++l) st16<true>(q.out + static_cast<uint64_t>(l) * q.cs, col, len, unpack_row<NW>(acc, l));
+}
+
+template <int NW, int LOCAL>
+__device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base) {
+  for (unsigned long long c0 = 0; c0 < q.len; c0 += kTileBytes) {
+    const uint32_t col = static_cast<uint32_t>(c0) + threadIdx.x * kLaneBytes;
+    if (static_cast<unsigned long long>(col) + kLaneBytes <= q.len)
+      svc_columns<NW, LOCAL, false>(q, lds_base, col);
+    else if (col < q.len)
+      svc_columns<NW, LOCAL, true>(q, lds_base, col);
+  }
+}
+
+template <int NW>
+__device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base) {
+  if (q.local_mode == kLocalXor)
+    svc_local<NW, kLocalXor>(q, lds_base);
+  else if (q.local_mode == kLocalZero)
+    svc_local<NW, kLocalZero>(q, lds_base);
+  else
+    svc_local<NW, kLocalNone>(q, lds_base);
+}
+
+// Workgroup b serves slot b. Wave 0 polls (relaxed system-scope loads: no
+// cache invalidation per poll) and publishes what it found in LDS word `cmd`
+// (0 keep polling, 1 serve, 2 leave); the whole workgroup acts on it, so every
+// exit path (stop flag, all slots idle, lifetime) is taken by every wave. A
+// request's tables stay staged in LDS while the next request uses the same
+// codec (same table address).
+__global__ __launch_bounds__(kBlock) void service_kernel(SvcCtl* ctl, SvcDev* st, unsigned long long epoch,
+                                                         unsigned long long idle_ticks, unsigned long long life_ticks) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  SvcReq* req = reinterpret_cast<SvcReq*>(lds + kSvcLds);
+  unsigned long long* cmd = reinterpret_cast<unsigned long long*>(lds + kSvcLds + sizeof(SvcReq));
+  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  SvcSlot* slot = &ctl->slot[blockIdx.x];
+  const bool poller = threadIdx.x < 64;  // wave 0
+  unsigned long long last = poller ? sys_load(&slot->done) : 0;
+  const unsigned long long t0 = static_cast<unsigned long long>(wall_clock64());
+  const uint4* staged = nullptr;  // tables in LDS (uniform)
+  int staged_n16 = 0;
+  for (;;) {
+    if (poller) {
+      unsigned long long action = 0, seq = 0;
+      for (int spin = 0; spin < 256 && action == 0; ++spin) {
+        seq = sys_load_relaxed(&slot->seq);
+        if (seq != last) {
+          action = 1;
+        } else if (sys_load_relaxed(&ctl->stop)) {
+          action = 2;
+        } else {
+          const unsigned long long now = static_cast<unsigned long long>(wall_clock64());
+          const unsigned long long act = __hip_atomic_load(&st->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (now - (act > t0 ? act : t0) > idle_ticks || now - t0 > life_ticks) action = 2;
+          else __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      if (action == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request and its blocks are visible
+        if (threadIdx.x < kSvcReqWords)
+          reinterpret_cast<unsigned long long*>(req)[threadIdx.x] =
+              sys_load_relaxed(reinterpret_cast<const unsigned long long*>(&slot->tbl) + threadIdx.x);
+      }
+      if (threadIdx.x == 0) {
+        cmd[0] = action;
+        cmd[1] = seq;
+      }
+    }
+    __syncthreads();
+    const unsigned long long action = cmd[0];
+    if (action == 2) break;
+    if (action == 1) {
+      const SvcReq& q = *req;  // read from LDS (a private copy would live in scratch)
+      const int n16 = q.k * 8 * q.nw;
+      if (q.tbl != staged || n16 != staged_n16) {
+        for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = q.tbl[i];
+        staged = q.tbl;
+        staged_n16 = n16;
+        __syncthreads();
+      }
+      if (q.nw == 2)
+        svc_request<2>(q, lds_base);
+      else
+        svc_request<1>(q, lds_base);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's parities are visible
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        sys_store(&slot->done, cmd[1]);
+        __hip_atomic_fetch_max(&st->last_active, static_cast<unsigned long long>(wall_clock64()), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (poller) last = cmd[1];
+    }
+    __syncthreads();  // cmd and req are rewritten next round
+  }
+  if (threadIdx.x == 0 &&
+      __hip_atomic_fetch_add(&st->exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x)
+    sys_store(&ctl->exited_epoch, epoch);  // the last workgroup out
+}
+
 }  // namespace
+
+hipError_t launch_service(SvcCtl* d_ctl, SvcDev* d_state, unsigned long long epoch, unsigned long long idle_ticks,
+                          unsigned long long life_ticks, hipStream_t s) {
+  (void)hipGetLastError();
+  hipLaunchKernelGGL(service_kernel, dim3(kSvcSlots), dim3(kBlock), kSvcLds + 128, s, d_ctl, d_state, epoch,
+                     idle_ticks, life_ticks);
+  return hipGetLastError();
+}
 
 hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
                              TicketCounter* tc) {

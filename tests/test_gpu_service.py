@@ -1,0 +1,112 @@
+"""The small-stripe request service (ecw_codec.cpp svc::, ecw_kernels.hip
+service_kernel): synchronous small host-memory encodes served by a resident
+kernel polling pinned memory — ECWide-H's one-4 KiB-chunk-per-call pattern
+(ECWide-H/proxy/encode.cpp:145-175). Bit-exact vs the oracle for every code
+shape it takes, from many threads at once, across its idle exit and relaunch,
+and the process leaves cleanly right after a call."""
+import os
+import subprocess
+import sys
+import threading
+import time
+
+import numpy as np
+import pytest
+
+from conftest import REPO, golden_blocks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def E():
+    import torch
+
+    assert torch.cuda.is_available()
+    import ecwide_amd
+
+    return ecwide_amd
+
+
+@pytest.mark.parametrize("code,k,m,r,ln,literal", [
+    ("R", 11, 3, 0, 4096, False),        # ECWide-H g_encode
+    ("C", 32, 3, 11, 4096, False),       # default scheme.ini shape, XOR locals
+    ("C", 32, 3, 11, 4096 + 37, True),   # ragged length, ECWide-C literal zero locals
+    ("C", 20, 6, 4, 3 * 4096 + 16, False),  # 5-8 global rows (u64 tables)
+    ("C", 200, 3, 40, 8192, False),      # > 16 rows per lane round
+    ("R", 5, 1, 0, 1, False),            # one byte
+    ("C", 128, 3, 27, 64 << 10, False),  # the service's largest block
+])
+def test_service_encode_vs_oracle(E, orc, code, k, m, r, ln, literal):
+    if code == "R":
+        c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(k, m, ln))
+    else:
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, ln), 1, False,
+                                     local_mode="literal" if literal else "xor")
+    oc = orc.codec(code, k, m, r if r else k, ln)
+    for rep in range(3):
+        data = [orc.fill(ln, 900 + rep, rep, j) for j in range(k)]
+        par = [np.full(ln, 0xA5, np.uint8) for _ in range(c.parityNum)]
+        c.encodeData(data, par)
+        want = oc.encode(data, literal=literal)
+        for i, w in enumerate(want):
+            assert np.array_equal(par[i], w), (rep, i)
+
+
+def test_service_golden_g_encode(E, orc, manifest):
+    """The ECWide-H g_encode golden vector through the service."""
+    h = manifest["ecwide_h"]
+    gd = [orc.fill(4096, 42, 0, j) for j in range(11)]
+    c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 4096))
+    par = [np.zeros(4096, np.uint8) for _ in range(3)]
+    c.encodeData(gd, par)
+    assert all(np.array_equal(a, b) for a, b in zip(par, golden_blocks(h["g_encode"], 3, 4096)))
+
+
+def test_service_many_threads_and_idle_relaunch(E, orc):
+    """20 threads (more than the 16 slots) x 40 calls on two codecs; then an
+    idle gap longer than the service's idle exit, and more calls (relaunch)."""
+    codecs = [(E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 4096)), orc.codec("R", 11, 3, 11, 4096)),
+              (E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(16, 2, 4, 4096), 1, False),
+               orc.codec("C", 16, 2, 4, 4096))]
+    errors = []
+
+    def worker(t):
+        c, oc = codecs[t % 2]
+        for n in range(40):
+            data = [orc.fill(4096, t, n, j) for j in range(c.encodeDataNum)]
+            par = [np.zeros(4096, np.uint8) for _ in range(c.parityNum)]
+            c.encodeData(data, par)
+            if not all(np.array_equal(a, b) for a, b in zip(par, oc.encode(data))):
+                errors.append((t, n))
+
+    for phase in range(2):
+        th = [threading.Thread(target=worker, args=(t,)) for t in range(20)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        assert not errors, errors[:5]
+        time.sleep(0.2)  # > the 20 ms idle exit: the next phase relaunches the service
+
+
+def test_service_then_device_sync_and_clean_exit(E, orc):
+    """A device synchronize right after service calls returns (the resident
+    kernel leaves when idle), and a process that exits right after a call
+    leaves cleanly (the service is stopped before the runtime goes)."""
+    import torch
+
+    c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 4096))
+    data = [orc.fill(4096, 1, 0, j) for j in range(11)]
+    par = [np.zeros(4096, np.uint8) for _ in range(3)]
+    c.encodeData(data, par)
+    t = time.perf_counter()
+    torch.cuda.synchronize()
+    assert time.perf_counter() - t < 5.0
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np, ecwide_amd as E\n"
+            "c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 4096))\n"
+            "d = [np.full(4096, j, np.uint8) for j in range(11)]; p = [np.zeros(4096, np.uint8) for _ in range(3)]\n"
+            "c.encodeData(d, p); print('ok', int(p[0].sum()))\n") % REPO
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0 and p.stdout.startswith("ok"), p.stderr[-2000:]

@@ -4,6 +4,7 @@ can link it instead of libisal."""
 import ctypes
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -18,6 +19,10 @@ _u8pp = ctypes.POINTER(_u8p)
 
 @pytest.fixture(scope="module")
 def shim():
+    return load_shim()
+
+
+def load_shim():
     import ecwide_amd  # noqa: F401  (torch-first runtime order, then the engine)
 
     L = ctypes.CDLL(SHIM)
@@ -168,8 +173,24 @@ def test_encode_stripes_batch(orc, S):
 @pytest.mark.gpu
 def test_ec_encode_data_concurrent_callers(shim, orc):
     """ECWide-H calls ec_encode_data from several proxy threads at once
-    (proxy.cpp:2001-2012): concurrent calls are batched into one GPU launch
-    (group commit) and every caller still gets exactly its own parities."""
+    (proxy.cpp:2001-2012): each call is served on a slot of its own by the
+    resident request service, and every caller gets exactly its own parities."""
+    concurrent_callers(shim, orc)
+
+
+@pytest.mark.gpu
+def test_ec_encode_data_concurrent_callers_batched():
+    """The same with the service off (ECW_SERVICE=0, read once per process, so
+    in a child process): concurrent calls are group-committed into launches."""
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import ecwide_amd, oracle, test_isal_shim as t\n"
+            "t.concurrent_callers(t.load_shim(), oracle.Oracle()); print('ok')\n") % (REPO, os.path.join(REPO, "tests"))
+    env = dict(os.environ, ECW_SERVICE="0")
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stderr[-3000:]
+
+
+def concurrent_callers(shim, orc):
     import threading
 
     k, m = 11, 3
