@@ -625,7 +625,7 @@ def main():
     if os.path.exists(args.pmc):
         try:
             pmc = json.load(open(args.pmc))
-            key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + (f"_tiled{args.chunk_kib}k" if args.layout == "tiled" else "")
+            key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{args.chunk_kib}k", "split": "_split"}.get(args.layout, "")
             ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
             traffic = ratio * enc_bytes / launches if ratio else None  # PMC bytes of one launch
         except Exception:
