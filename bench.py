@@ -20,8 +20,8 @@ Multi-GPU: `python bench.py --gpus N` starts N rank processes itself
 (torch.distributed.run in a child process, before any GPU call in this one)
 unless it already runs under torch.distributed.run. One process per GPU; each
 rank owns its stripes in its own HBM, no data moves between GPUs;
-torch.distributed (RCCL) only lines ranks up (barrier) and takes the max of
-the per-rank times.
+torch.distributed (gloo: there is no data exchange to put on RCCL) only lines
+ranks up (barrier) and takes the max of the per-rank times.
 """
 from __future__ import annotations
 
@@ -139,17 +139,17 @@ class Dist:
 
             if not self.distinct:
                 print(f"bench.py: rehearsal: {self.world} ranks share {self.ndev} GPU(s)", file=sys.stderr)
-            if self.dry or not self.distinct:
-                dist.init_process_group("gloo")
-            else:
-                dist.init_process_group("nccl", device_id=torch.device(f"cuda:{self.dev}"))
+            # no stripe byte moves between ranks: the only collectives are the
+            # barriers around the timed region and a few scalars (max time, min
+            # block size, verification), so they run on gloo over loopback --
+            # the same on one GPU or eight, and no RCCL communicator is set up
+            dist.init_process_group("gloo")
             self.backend = dist.get_backend()
 
     def _tensor(self, vals):
         import torch
 
-        on_gpu = self.backend == "nccl"
-        return torch.tensor(vals, dtype=torch.float64, device=f"cuda:{self.dev}" if on_gpu else "cpu")
+        return torch.tensor(vals, dtype=torch.float64)
 
     def barrier(self):
         if self.world > 1:

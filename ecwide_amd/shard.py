@@ -4,8 +4,8 @@ the data path).
 Stripes are independent: a batch is split into contiguous
 stripe ranges, each rank encodes/repairs its own range from its own HBM.
 torch.distributed is used only to line ranks up for timing (barrier) and to
-take the max of the per-rank times; with the nccl backend that is RCCL, but
-no stripe byte ever crosses xGMI.
+take the max of the per-rank times (bench.py runs those on gloo); no stripe
+byte ever crosses xGMI.
 """
 from __future__ import annotations
 
