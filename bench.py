@@ -371,9 +371,11 @@ def other_layouts(args, E, codec, S, B, s0, out, enc_bytes, rep_bytes, dev) -> d
             blk.random_(0, 256, generator=gen)
     batch = E.BlockBatch(codec, data, par)
     enc = timed(batch.encode, enc_bytes)
+    outs = [out[s_ * B:(s_ + 1) * B] for s_ in range(S)]
+    rep = timed(lambda: batch.repair(0, outs), rep_bytes)
     res["pointer"] = {"layout": f"pointer mode: {S * (k + np_)} separately allocated {B >> 20} MiB blocks, one "
-                                f"ecw_encode_ptrs_dev launch over the {S} stripes", "steps": n2, "encode_GBps": enc,
-                      "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
+                                f"ecw_encode_ptrs_dev / ecw_xor_reduce_ptrs_dev launch over the {S} stripes",
+                      "steps": n2, "encode_GBps": enc, "repair_GBps": rep, "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
     return res
 
 

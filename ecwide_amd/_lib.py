@@ -81,6 +81,7 @@ SIGNATURES = {
     "ecw_partial_decode_dev": (c_int, [c_void_p, _pp, c_void_p, c_size_t, c_void_p]),
     "ecw_xor_intermediate_dev": (c_int, [c_void_p, _pp, _pp, c_size_t, c_void_p]),
     "ecw_xor_reduce_dev": (c_int, [c_int, _pp, c_int, c_void_p, c_size_t, c_void_p]),
+    "ecw_xor_reduce_ptrs_dev": (c_int, [c_int, c_int, c_int, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ecw_encode_batch_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_size_t, c_void_p]),
     "ecw_encode_batch_split_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_void_p, c_size_t, c_size_t,
                                            c_int, c_size_t, c_void_p]),

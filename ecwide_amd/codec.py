@@ -315,6 +315,34 @@ class BlockBatch:
     def encode_bytes(self) -> int:
         return self.stripes * (self.codec.encodeDataNum + self.codec.parityNum) * self.len
 
+    def repair(self, lost_block: int, out, stream=None) -> None:
+        """CL single-block repair of `lost_block` (stripe block index: D_j = j,
+        L_t = k + m + t) of every stripe into out[s] (HBM tensors), as the XOR of
+        its surviving group members (ecw_repair_sources), one launch for the
+        batch (ecw_xor_reduce_ptrs_dev)."""
+        import torch
+
+        if len(out) != self.stripes:
+            raise ValueError(f"need {self.stripes} output blocks")
+        k = self.codec.encodeDataNum
+        srcs = self.codec.repairSources(lost_block)
+        key = (lost_block, tuple(_addr(o) for o in out))
+        if getattr(self, "_rkey", None) != key:
+            blocks = [self._keep[s * k:(s + 1) * k] + self._keep[self.stripes * k + s * self.codec.parityNum:
+                                                                 self.stripes * k + (s + 1) * self.codec.parityNum]
+                      for s in range(self.stripes)]
+            dev = self.dtab.device
+            self._rsrc = torch.tensor([_addr(blocks[s][i]) for s in range(self.stripes) for i in srcs],
+                                      dtype=torch.int64, device=dev)
+            self._rdst = torch.tensor([_addr(o) for o in out], dtype=torch.int64, device=dev)
+            self._rkeep, self._rkey = list(out), key
+        _check(lib.ecw_xor_reduce_ptrs_dev(self.codec.device, self.stripes, len(srcs), c_void_p(self._rsrc.data_ptr()),
+                                           c_void_p(self._rdst.data_ptr()), self.len,
+                                           stream if stream is not None else _stream()), "repair")
+
+    def repair_bytes(self, lost_block: int) -> int:
+        return self.stripes * (len(self.codec.repairSources(lost_block)) + 1) * self.len
+
 
 def xor_reduce(src, dst, length=None, device: int = 0) -> None:
     """dst = XOR of the device blocks in `src` (any fan-in 1..256)."""

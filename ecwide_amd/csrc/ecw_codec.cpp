@@ -642,6 +642,18 @@ int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* 
   return run_xor_ptr(d_src, n, d_dst, len, static_cast<hipStream_t>(stream));
 }
 
+int ecw_xor_reduce_ptrs_dev(int device, int stripes, int n, const uint8_t* const* d_src_ptrs,
+                            uint8_t* const* d_dst_ptrs, size_t len, void* stream) {
+  if (!d_src_ptrs || !d_dst_ptrs || stripes < 0 || n < 1 || n > kMaxSrc || !check_len(len)) return ECW_EINVAL;
+  if (reinterpret_cast<uintptr_t>(d_src_ptrs) % 8 || reinterpret_cast<uintptr_t>(d_dst_ptrs) % 8) return ECW_EALIGN;
+  if (len == 0 || stripes == 0) return ECW_OK;
+  DeviceGuard g(device);
+  if (!g.ok) return ECW_EDEVICE;
+  const XorTab t{d_src_ptrs, d_dst_ptrs, n};
+  const XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
+  return status_of(launch_xor_tab(t, xg, static_cast<hipStream_t>(stream)));
+}
+
 int ecw_decode_dev(ecw_codec* c, const uint8_t* const* d_data, uint8_t* d_target, size_t len, void* stream) {
   if (!c) return ECW_EINVAL;
   return ecw_xor_reduce_dev(c->device, d_data, c->info.decode_data_num, d_target, len, stream);

@@ -112,6 +112,13 @@ struct XorSplit {
   int ndata;
   int idx[kMaxSrc];              // block index of source i within its region
 };
+// Device pointer tables (ecw_xor_reduce_ptrs_dev): source i of stripe s at
+// src[s*n + i], its output at dst[s].
+struct XorTab {
+  const uint8_t* const* src;
+  uint8_t* const* dst;
+  int n;
+};
 struct XorGeom {
   uint64_t len, tiles;
   int stripes, n;
@@ -119,6 +126,7 @@ struct XorGeom {
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s);
+hipError_t launch_xor_tab(const XorTab& p, const XorGeom& g, hipStream_t s);
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes,
                               int nblocks, uint64_t len, uint64_t piece, uint64_t pstride,

@@ -451,6 +451,10 @@ __device__ __forceinline__ const uint8_t* xsrc(const XorSplit& a, int s, int i) 
   if (i < a.ndata) return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
   return a.pbase + s * a.psstride + static_cast<uint64_t>(a.idx[i]) * a.pbstride;
 }
+__device__ __forceinline__ const uint8_t* xsrc(const XorTab& a, int s, int i) {
+  return a.src[static_cast<uint64_t>(s) * a.n + i];
+}
+__device__ __forceinline__ uint8_t* xdst(const XorTab& a, int s) { return a.dst[s]; }
 __device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
 __device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }
 __device__ __forceinline__ uint8_t* xdst(const XorSplit& a, int s) { return a.out + s * a.ostride; }
@@ -925,6 +929,7 @@ bool encode_uses_ticket(uint64_t tiles, int k) {
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
+hipError_t launch_xor_tab(const XorTab& p, const XorGeom& g, hipStream_t s) { return launch_xor(p, g, s); }
 
 hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, int stripes, int nblocks,
                               uint64_t len, uint64_t piece, uint64_t pstride, uint64_t offset, uint64_t seed,

@@ -214,6 +214,13 @@ int ecw_xor_intermediate_dev(ecw_codec* codec, const uint8_t* const* d_source,
  * ECW_EUNSUPPORTED here. */
 int ecw_encode_ptrs_dev(ecw_codec* codec, int stripes, const uint8_t* const* d_data_ptrs,
                         uint8_t* const* d_parity_ptrs, size_t len, void* stream);
+/* dst[s] = XOR of src[s*n + 0 .. s*n + n-1] for every stripe s, one launch: the
+ * decode / partial decode / CL repair of a batch of stripes whose blocks are
+ * separately placed (d_src_ptrs, d_dst_ptrs: DEVICE arrays of block pointers,
+ * 8-byte aligned; every block `len` bytes, 16-byte aligned). n in [1, 256].
+ * The sources of a CL repair are ecw_repair_sources' blocks. */
+int ecw_xor_reduce_ptrs_dev(int device, int stripes, int n, const uint8_t* const* d_src_ptrs,
+                            uint8_t* const* d_dst_ptrs, size_t len, void* stream);
 /* target = XOR of n device blocks (the arithmetic of decode / partial decode
  * / relayer stage for any fan-in); n in [1, 256]. */
 int ecw_xor_reduce_dev(int device, const uint8_t* const* d_src, int n, uint8_t* d_dst, size_t len,

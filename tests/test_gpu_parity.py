@@ -383,6 +383,52 @@ def test_encode_ptrs_dev_vs_oracle(E, torch, orc, k, m, r, B, S, local):
             assert (got[B:] == 0x5A).all(), ("wrote past the block", s, i)
 
 
+@pytest.mark.parametrize("n,ln,S", [(1, 4096, 2), (27, 3 * 4096 + 48, 3), (33, 8192, 2), (64, 5000, 2)])
+def test_xor_reduce_ptrs_dev_vs_oracle(E, torch, orc, n, ln, S):
+    """ecw_xor_reduce_ptrs_dev: dst[s] = XOR of n separately allocated blocks,
+    every stripe in one launch (straight-line kernel up to 32 sources, the ring
+    kernel beyond), ragged tails, nothing written past the block."""
+    from ctypes import c_void_p
+
+    from ecwide_amd._lib import lib
+
+    data = [[orc.fill(ln, 70 + s, s, i) for i in range(n)] for s in range(S)]
+    src = [[torch.from_numpy(d).cuda() for d in row] for row in data]
+    dst = [torch.full((ln + 32,), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(S)]
+    st = torch.tensor([b.data_ptr() for row in src for b in row], dtype=torch.int64, device="cuda")
+    dt = torch.tensor([d.data_ptr() for d in dst], dtype=torch.int64, device="cuda")
+    assert lib.ecw_xor_reduce_ptrs_dev(0, S, n, c_void_p(st.data_ptr()), c_void_p(dt.data_ptr()), ln,
+                                       c_void_p(torch.cuda.current_stream().cuda_stream)) == 0
+    torch.cuda.synchronize()
+    for s in range(S):
+        got = dst[s].cpu().numpy()
+        assert np.array_equal(got[:ln], orc.xor_blocks(data[s])), s
+        assert (got[ln:] == 0x5A).all(), s
+
+
+def test_block_batch_encode_repair(E, torch, orc):
+    """BlockBatch: a batch of stripes of separately allocated blocks, encoded and
+    every D and L block repaired through device pointer tables, one launch each."""
+    k, m, r, B, S = 40, 3, 9, 3 * 8192, 3
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    data = [[torch.from_numpy(orc.fill(B, 12, s, j)).cuda() for j in range(k)] for s in range(S)]
+    par = [[torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(c.parityNum)] for _ in range(S)]
+    batch = E.BlockBatch(c, data, par)
+    batch.encode()
+    oc = orc.codec("C", k, m, r, B)
+    torch.cuda.synchronize()
+    for s in range(S):
+        want = oc.encode([d.cpu().numpy() for d in data[s]])
+        assert all(np.array_equal(p.cpu().numpy(), w) for p, w in zip(par[s], want)), s
+    out = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(S)]
+    for lost in list(range(0, k, 7)) + [k - 1] + [k + m + t for t in range(c.groupNum)]:
+        batch.repair(lost, out)
+        torch.cuda.synchronize()
+        for s in range(S):
+            want = data[s][lost] if lost < k else par[s][lost - k]
+            assert torch.equal(out[s], want), (lost, s)
+
+
 def test_encode_ptrs_dev_ticket_and_errors(E, torch, orc):
     """>= 262,144 tiles through the pointer tables take the ticket-ordered
     launch (twice on one stream: the counter carries over); the result equals
