@@ -1110,7 +1110,8 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
       sv->broken = true;
       return kNotServed;
     }
-    sv->cv.wait(lk, [&] { return !sv->free_slots.empty(); });
+    sv->cv.wait(lk, [&] { return !sv->free_slots.empty() || sv->broken; });
+    if (sv->broken) return kNotServed;
     slot = sv->free_slots.back();
     sv->free_slots.pop_back();
     if (sv->ensure_stage(slot, cs * (k + np)) != ECW_OK) {
@@ -1119,10 +1120,11 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
       return kNotServed;
     }
   }
+  // give the slot back (takes mu: never call it with mu held)
   auto release = [&](int st) {
     std::lock_guard<std::mutex> lk(sv->mu);
     sv->free_slots.push_back(slot);
-    sv->cv.notify_one();
+    sv->cv.notify_all();
     return st;
   };
   uint8_t* h = sv->stage[slot];
@@ -1142,14 +1144,15 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
   q.nw = nw;
   const unsigned long long seq = q.seq + 1;  // only this thread writes the slot while it holds it
   __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
+  bool up;
   {
     std::lock_guard<std::mutex> lk(sv->mu);
-    if (sv->ensure_running() != ECW_OK) {
-      sv->broken = true;
-      return release(ECW_EDEVICE);
-    }
+    up = sv->ensure_running() == ECW_OK;
+    if (!up) sv->broken = true;  // the launch path takes this call and every later one
   }
+  if (!up) return release(kNotServed);
   const auto t0 = std::chrono::steady_clock::now();
+  int failed = ECW_OK;
   for (unsigned spins = 1; __atomic_load_n(&q.done, __ATOMIC_ACQUIRE) != seq; ++spins) {
     if (spins % 1024) {
       __builtin_ia32_pause();
@@ -1158,15 +1161,14 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     std::lock_guard<std::mutex> lk(sv->mu);
     if (__atomic_load_n(&q.done, __ATOMIC_ACQUIRE) == seq) break;
     // the epoch this request was posted to left before serving it: start the next one
-    if (sv->ensure_running() != ECW_OK) {
+    if (sv->ensure_running() != ECW_OK ||
+        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {  // 10 s: the device is gone
       sv->broken = true;
-      return release(ECW_EDEVICE);
-    }
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
-      sv->broken = true;  // a request that takes 10 s means the device is gone: stop using the service
-      return release(ECW_EDEVICE);
+      failed = ECW_EDEVICE;
+      break;
     }
   }
+  if (failed) return release(failed);
   for (int i = 0; i < np; ++i) std::memcpy(parity[i], h + static_cast<size_t>(k + i) * cs, len);
   return release(ECW_OK);
 }
