@@ -1073,9 +1073,31 @@ struct Service {
 std::mutex g_mu;
 std::map<int, Service*> g_services;  // one per device, kept for the life of the process
 
+#ifndef ECW_SVC_TRACE
+#define ECW_SVC_TRACE 0  // tools only (tools/variants.py): per-phase latency of served calls, printed at exit
+#endif
+#if ECW_SVC_TRACE
+// host ns: copy in, post -> done seen, copy out; device ticks: detect -> words,
+// words -> start, start -> computed, computed -> fenced
+double g_tr[7] = {};
+unsigned long long g_tr_n = 0;
+#endif
+
 void stop_all() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& kv : g_services) kv.second->stop();
+#if ECW_SVC_TRACE
+  if (g_tr_n) {
+    int khz = 100000;
+    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
+    const double n = static_cast<double>(g_tr_n), tick_us = 1e3 / khz;
+    std::fprintf(stderr,
+                 "svc trace (%llu calls, us): copy-in %.2f  post->done %.2f  copy-out %.2f | device: part 0 saw it -> "
+                 "the last part saw it %.2f  -> start %.2f  -> computed %.2f  -> fenced %.2f\n",
+                 g_tr_n, g_tr[0] / n / 1e3, g_tr[1] / n / 1e3, g_tr[2] / n / 1e3, g_tr[3] / n * tick_us,
+                 g_tr[4] / n * tick_us, g_tr[5] / n * tick_us, g_tr[6] / n * tick_us);
+  }
+#endif
 }
 
 Service* service_for(int device) {
@@ -1128,21 +1150,39 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     return st;
   };
   uint8_t* h = sv->stage[slot];
+#if ECW_SVC_TRACE
+  const auto tr0 = std::chrono::steady_clock::now();
+#endif
   for (int j = 0; j < k; ++j) std::memcpy(h + j * cs, data[j], len);
+#if ECW_SVC_TRACE
+  const auto tr1 = std::chrono::steady_clock::now();
+#endif
   SvcSlot& q = sv->ctl->slot[slot];
-  q.tbl = c->d_pass[0];
-  q.data = sv->d_stage[slot];
-  q.out = sv->d_stage[slot] + static_cast<size_t>(k) * cs;
-  q.len = len;
-  q.cs = cs;
-  q.k = k;
-  q.nrows = m;
-  q.m = m;
-  q.r = c->has_local() ? c->r() : k;
-  q.groups = c->groups();
-  q.local_mode = local_mode_of(c);
-  q.nw = nw;
-  const unsigned long long seq = q.seq + 1;  // only this thread writes the slot while it holds it
+  // only this thread writes the slot while it holds it
+  const SvcSlot want = [&] {
+    SvcSlot w = q;
+    w.tbl = c->d_pass[0];
+    w.data = sv->d_stage[slot];
+    w.out = sv->d_stage[slot] + static_cast<size_t>(k) * cs;
+    w.len = len;
+    w.cs = cs;
+    w.k = k;
+    w.nrows = m;
+    w.m = m;
+    w.r = c->has_local() ? c->r() : k;
+    w.groups = c->groups();
+    w.local_mode = local_mode_of(c);
+    w.nw = nw;
+    return w;
+  }();
+  constexpr unsigned long long kSeqMask = (1ull << kSvcSeqBits) - 1;
+  unsigned long long gen = q.seq >> kSvcSeqBits;
+  const size_t words = offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl);
+  if (q.seq == 0 || std::memcmp(&want.tbl, &q.tbl, words) != 0) {  // new request words: a new generation
+    std::memcpy(&q.tbl, &want.tbl, words);
+    gen = (gen + 1) & ((1ull << (64 - kSvcSeqBits)) - 1);
+  }
+  const unsigned long long seq = (gen << kSvcSeqBits) | (((q.seq & kSeqMask) + 1) & kSeqMask);
   __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
   bool up;
   {
@@ -1169,7 +1209,22 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     }
   }
   if (failed) return release(failed);
+#if ECW_SVC_TRACE
+  const auto tr2 = std::chrono::steady_clock::now();
+#endif
   for (int i = 0; i < np; ++i) std::memcpy(parity[i], h + static_cast<size_t>(k + i) * cs, len);
+#if ECW_SVC_TRACE
+  {
+    const auto tr3 = std::chrono::steady_clock::now();
+    auto ns = [](auto d) { return static_cast<double>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
+    std::lock_guard<std::mutex> lk(g_mu);
+    g_tr[0] += ns(tr1 - tr0);
+    g_tr[1] += ns(tr2 - tr1);
+    g_tr[2] += ns(tr3 - tr2);
+    for (int i = 0; i < 4; ++i) g_tr[3 + i] += static_cast<double>(q.pad1[i + 1] - q.pad1[i]);
+    ++g_tr_n;
+  }
+#endif
   return release(ECW_OK);
 }
 

@@ -137,10 +137,10 @@ int device_cu_count(int device);
 // ---- small-stripe request service (ecw_codec.cpp: svc::) -------------------
 // A resident kernel serves synchronous small encodes (ECWide-H encodes one
 // 4 KiB chunk per ec_encode_data call, ECWide-H/proxy/encode.cpp:145-175)
-// without a launch or a stream synchronisation per call: workgroup i polls
-// slot i of a control block in coherent pinned host memory, reads the
-// request's blocks from pinned staging over PCIe, writes the parities back
-// there and publishes `done`. Every workgroup leaves the loop on the stop flag,
+// without a launch or a stream synchronisation per call: the workgroups of
+// slot i poll slot i of a control block in coherent pinned host memory, read
+// the request's blocks from pinned staging over PCIe, write the parities back
+// there and publish `done`. Every workgroup leaves the loop on the stop flag,
 // once NO slot has had a request for `idle_ticks` of wall clock, or after
 // `life_ticks`; the last one out publishes exited_epoch = epoch, and the host
 // launches the next epoch when a request finds the service gone.
@@ -148,12 +148,18 @@ constexpr int kSvcSlots = 16;  // concurrent callers served at once (one workgro
 constexpr size_t kSvcMaxLen = size_t(64) << 10;   // bytes per block served (larger: launch path)
 constexpr size_t kSvcLds = size_t(60) << 10;       // LDS for the packed tables: k * 128 * nw bytes
 
+// `seq` and `done` hold a request word: the request number in the low
+// kSvcSeqBits bits, the generation of the request words below in the bits
+// above. The host bumps the generation only when the request words change
+// (another codec, length or staging), so a workgroup that already holds that
+// generation skips reading them: one PCIe round trip less per call.
+constexpr int kSvcSeqBits = 40;
 struct alignas(64) SvcSlot {
-  unsigned long long seq;    // host: number of the latest request
+  unsigned long long seq;    // host: word of the latest request
   unsigned long long pad0[7];
-  unsigned long long done;   // device: number of the latest finished request
+  unsigned long long done;   // device: word of the latest finished request
   unsigned long long pad1[7];
-  // the request (written by the host before `seq`)
+  // the request words (written by the host before `seq` when they change)
   const void* tbl;           // packed tables of the codec's pass 0 (device memory)
   uint8_t* data;             // k input rows, `cs` bytes apart (device view of pinned staging)
   uint8_t* out;              // parity rows [G.., L..], `cs` bytes apart
@@ -169,9 +175,25 @@ struct SvcCtl {
 };
 
 // device-memory state of one service launch (zeroed before every launch)
+// Each slot is served by kSvcParts single-wave workgroups, each taking every
+// kSvcParts-th 1 KiB column chunk: one wave reads pinned host memory at ~2 GB/s
+// (a 4 KiB k=11 call: 20.5 us of loads with 1 part, 2.8 us with 8), so a call's
+// blocks come in through 8 waves at once. Every part polls the slot; the last
+// part to finish publishes `done`.
+#ifndef ECW_SVC_PARTS
+#define ECW_SVC_PARTS 8
+#endif
+constexpr int kSvcParts = ECW_SVC_PARTS;
+constexpr int kSvcWave = 64;  // threads per service workgroup (one wave)
 struct SvcDev {
   unsigned long long last_active;  // wall clock of the latest request served by any workgroup
   unsigned int exited;             // workgroups that left the loop
+  unsigned int pad;
+  struct Slot {
+    unsigned long long seq;        // kSvcLeave once part 0 has left (tells the other parts)
+    unsigned int fin;              // parts finished (monotonic; the one that makes it a multiple of kSvcParts publishes)
+    unsigned int pad[13];
+  } slot[kSvcSlots];
 };
 
 hipError_t launch_service(SvcCtl* d_ctl, SvcDev* d_state, unsigned long long epoch, unsigned long long idle_ticks,

@@ -739,6 +739,9 @@ hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
 }
 
 // ---- small-stripe request service (ecw_internal.hpp SvcCtl) ----------------
+#ifndef ECW_SVC_TRACE
+#define ECW_SVC_TRACE 0  // tools only: wall-clock stamps of each request's phases (ecw_codec.cpp svc::)
+#endif
 __device__ __forceinline__ unsigned long long sys_load(const unsigned long long* p) {
   return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -763,9 +766,8 @@ static_assert(offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl) == 
 
 // One lane's 16 columns of a served request. All input rows of a round of 16
 // are loaded before the first product: they come from pinned host memory, so
-// one PCIe round trip per 16 rows, not one per ring slot. Full lanes load every
-// row of the round unconditionally (rows past k re-read row k-1) with the
-// volatile buffer load, so the compiler keeps all 16 loads in flight.
+// one PCIe round trip per 16 rows, not one per ring slot (the volatile buffer
+// load keeps the compiler from sinking them to their uses).
 template <int NW, int LOCAL, bool TAIL>
 __device__ __forceinline__ void svc_columns(const SvcReq& q, uint32_t lds_base, uint32_t col) {
   const uint32_t len = static_cast<uint32_t>(q.len);
@@ -778,10 +780,8 @@ __device__ __forceinline__ void svc_columns(const SvcReq& q, uint32_t lds_base, 
   for (int j0 = 0; j0 < k; j0 += 16) {
     uint4 v[16];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const uint8_t* row = q.data + static_cast<uint64_t>(j0 + u < k ? j0 + u : k - 1) * q.cs;
-      v[u] = ld16<TAIL>(uniform_ptr(row), col, len);
-    }
+    for (int u = 0; u < 16; ++u)
+      if (j0 + u < k) v[u] = ld16<TAIL>(uniform_ptr(q.data + static_cast<uint64_t>(j0 + u) * q.cs), col, len);
 #pragma unroll
     for (int u = 0; u < 16; ++u) {
       const int j = j0 + u;
@@ -802,9 +802,12 @@ __device__ __forceinline__ void svc_columns(const SvcReq& q, uint32_t lds_base, 
   for (int l = 0; l < q.nrows; ++l) st16<true>(q.out + static_cast<uint64_t>(l) * q.cs, col, len, unpack_row<NW>(acc, l));
 }
 
+// this workgroup's column chunks (1 KiB: 64 lanes x 16 B) of a request
 template <int NW, int LOCAL>
-__device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base) {
-  for (unsigned long long c0 = 0; c0 < q.len; c0 += kTileBytes) {
+__device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base, int part) {
+  constexpr uint32_t kChunk = kSvcWave * kLaneBytes;
+  for (unsigned long long c0 = static_cast<unsigned long long>(part) * kChunk; c0 < q.len;
+       c0 += static_cast<unsigned long long>(kSvcParts) * kChunk) {
     const uint32_t col = static_cast<uint32_t>(c0) + threadIdx.x * kLaneBytes;
     if (static_cast<unsigned long long>(col) + kLaneBytes <= q.len)
       svc_columns<NW, LOCAL, false>(q, lds_base, col);
@@ -814,87 +817,121 @@ __device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base) {
 }
 
 template <int NW>
-__device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base) {
+__device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base, int part) {
   if (q.local_mode == kLocalXor)
-    svc_local<NW, kLocalXor>(q, lds_base);
+    svc_local<NW, kLocalXor>(q, lds_base, part);
   else if (q.local_mode == kLocalZero)
-    svc_local<NW, kLocalZero>(q, lds_base);
+    svc_local<NW, kLocalZero>(q, lds_base, part);
   else
-    svc_local<NW, kLocalNone>(q, lds_base);
+    svc_local<NW, kLocalNone>(q, lds_base, part);
 }
 
-// Workgroup b serves slot b. Wave 0 polls (relaxed system-scope loads: no
-// cache invalidation per poll) and publishes what it found in LDS word `cmd`
-// (0 keep polling, 1 serve, 2 leave); the whole workgroup acts on it, so every
-// exit path (stop flag, all slots idle, lifetime) is taken by every wave. A
-// request's tables stay staged in LDS while the next request uses the same
-// codec (same table address).
-__global__ __launch_bounds__(kBlock) void service_kernel(SvcCtl* ctl, SvcDev* st, unsigned long long epoch,
-                                                         unsigned long long idle_ticks, unsigned long long life_ticks) {
+// Workgroup b (one wave) is part b % kSvcParts of slot b / kSvcParts. Every
+// part polls the slot's request word in host memory (relaxed system-scope
+// loads: no cache invalidation per poll; a hand-off from one poller through
+// device memory measured 2-6 us slower, the parts sitting on different XCDs)
+// and reads the request words when their generation changed. Each part
+// computes its column chunks, makes its parity stores visible (release,
+// system scope) and counts itself finished; the part that completes the count
+// publishes `done`.
+// Part 0 leaves on the stop flag, once NO slot has had a request for
+// `idle_ticks`, or after `life_ticks` (checked every 64th poll), and tells its
+// other parts so through device memory; the last workgroup out publishes
+// exited_epoch. A request posted as part 0 leaves waits for the next epoch
+// (the host relaunches on exited_epoch), which serves it whole. A request's tables stay staged in LDS
+// while the next request uses the same codec (same table address).
+constexpr unsigned long long kSvcLeave = ~0ull;  // SvcDev::Slot::seq: part 0 has left
+
+__global__ __launch_bounds__(kSvcWave) void service_kernel(SvcCtl* ctl, SvcDev* st, unsigned long long epoch,
+                                                           unsigned long long idle_ticks,
+                                                           unsigned long long life_ticks) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   SvcReq* req = reinterpret_cast<SvcReq*>(lds + kSvcLds);
-  unsigned long long* cmd = reinterpret_cast<unsigned long long*>(lds + kSvcLds + sizeof(SvcReq));
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
-  SvcSlot* slot = &ctl->slot[blockIdx.x];
-  const bool poller = threadIdx.x < 64;  // wave 0
-  unsigned long long last = poller ? sys_load(&slot->done) : 0;
+  const int si = blockIdx.x / kSvcParts, part = blockIdx.x % kSvcParts;
+  SvcSlot* slot = &ctl->slot[si];
+  SvcDev::Slot* ds = &st->slot[si];
   const unsigned long long t0 = static_cast<unsigned long long>(wall_clock64());
-  const uint4* staged = nullptr;  // tables in LDS (uniform)
+  // the request word this part last served
+  unsigned long long last = sys_load(&slot->done);
+  unsigned long long req_gen = ~0ull;  // generation of the request words held in LDS (none yet)
+  const uint4* staged = nullptr;       // tables in LDS
   int staged_n16 = 0;
+#if ECW_SVC_TRACE
+  unsigned long long trace[5] = {0, 0, 0, 0, 0};  // tools only: detect, words, start, computed, fenced
+#endif
   for (;;) {
-    if (poller) {
-      unsigned long long action = 0, seq = 0;
-      for (int spin = 0; spin < 256 && action == 0; ++spin) {
-        seq = sys_load_relaxed(&slot->seq);
-        if (seq != last) {
-          action = 1;
-        } else if (sys_load_relaxed(&ctl->stop)) {
-          action = 2;
-        } else {
-          const unsigned long long now = static_cast<unsigned long long>(wall_clock64());
-          const unsigned long long act = __hip_atomic_load(&st->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          if (now - (act > t0 ? act : t0) > idle_ticks || now - t0 > life_ticks) action = 2;
-          else __builtin_amdgcn_s_sleep(1);
+    // --- wait for a request: every part polls the slot's word in host memory
+    // (the whole wave loads the same word: uniform control flow) ---
+    unsigned long long seq = 0;
+    bool leave = false;
+    for (int spin = 1;; ++spin) {
+      seq = sys_load_relaxed(&slot->seq);
+      if (seq != last) break;
+      if ((spin & 63) == 0) {
+        // part 0 decides for its slot (idle, lifetime, stop) and tells the other
+        // parts through device memory; they watch that, the stop flag and the
+        // lifetime (plus a margin) only, as a safety net
+        const unsigned long long now = static_cast<unsigned long long>(wall_clock64());
+        const unsigned long long act = __hip_atomic_load(&st->last_active, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool idle = part == 0 && now - (act > t0 ? act : t0) > idle_ticks;
+        const bool told = part != 0 && __hip_atomic_load(&ds->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == kSvcLeave;
+        if (idle || told || sys_load_relaxed(&ctl->stop) || now - t0 > life_ticks + (part == 0 ? 0 : idle_ticks)) {
+          leave = true;
+          break;
         }
       }
-      if (action == 1) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request and its blocks are visible
-        if (threadIdx.x < kSvcReqWords)
-          reinterpret_cast<unsigned long long*>(req)[threadIdx.x] =
-              sys_load_relaxed(reinterpret_cast<const unsigned long long*>(&slot->tbl) + threadIdx.x);
-      }
-      if (threadIdx.x == 0) {
-        cmd[0] = action;
-        cmd[1] = seq;
-      }
     }
-    __syncthreads();
-    const unsigned long long action = cmd[0];
-    if (action == 2) break;
-    if (action == 1) {
-      const SvcReq& q = *req;  // read from LDS (a private copy would live in scratch)
-      const int n16 = q.k * 8 * q.nw;
-      if (q.tbl != staged || n16 != staged_n16) {
-        for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = q.tbl[i];
-        staged = q.tbl;
-        staged_n16 = n16;
-        __syncthreads();
-      }
-      if (q.nw == 2)
-        svc_request<2>(q, lds_base);
-      else
-        svc_request<1>(q, lds_base);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this wave's parities are visible
+    if (leave) {
+      if (part == 0 && threadIdx.x == 0) __hip_atomic_store(&ds->seq, kSvcLeave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }
+#if ECW_SVC_TRACE
+    trace[0] = trace[1] = trace[2] = static_cast<unsigned long long>(wall_clock64());
+#endif
+    // activity counts from the request's arrival, so part 0 never leaves on
+    // idle while one of its requests is still in flight
+    if (part == 0 && threadIdx.x == 0)
+      __hip_atomic_fetch_max(&st->last_active, static_cast<unsigned long long>(wall_clock64()), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request and its blocks are visible
+    const unsigned long long gen = seq >> kSvcSeqBits;
+    if (gen != req_gen) {  // new request words: 9 lanes read them at once
+      if (threadIdx.x < kSvcReqWords)
+        reinterpret_cast<unsigned long long*>(req)[threadIdx.x] =
+            sys_load_relaxed(reinterpret_cast<const unsigned long long*>(&slot->tbl) + threadIdx.x);
+      req_gen = gen;
       __syncthreads();
-      if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        sys_store(&slot->done, cmd[1]);
-        __hip_atomic_fetch_max(&st->last_active, static_cast<unsigned long long>(wall_clock64()), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-      }
-      if (poller) last = cmd[1];
     }
-    __syncthreads();  // cmd and req are rewritten next round
+    const SvcReq& q = *req;  // read from LDS (a private copy would live in scratch)
+    const int n16 = q.k * 8 * q.nw;
+    if (q.tbl != staged || n16 != staged_n16) {
+      for (int i = threadIdx.x; i < n16; i += kSvcWave) reinterpret_cast<uint4*>(lds)[i] = q.tbl[i];
+      staged = q.tbl;
+      staged_n16 = n16;
+      __syncthreads();
+    }
+    if (q.nw == 2)
+      svc_request<2>(q, lds_base, part);
+    else
+      svc_request<1>(q, lds_base, part);
+#if ECW_SVC_TRACE
+    trace[3] = static_cast<unsigned long long>(wall_clock64());
+#endif
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope: this part's parities are visible
+    last = seq;
+    if (threadIdx.x == 0 &&
+        (__hip_atomic_fetch_add(&ds->fin, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1) % kSvcParts == 0) {
+#if ECW_SVC_TRACE
+      trace[4] = static_cast<unsigned long long>(wall_clock64());
+      for (int i = 0; i < 5; ++i) __hip_atomic_store(&slot->pad1[i], trace[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#endif
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      sys_store(&slot->done, seq);  // the last part of this request
+      __hip_atomic_fetch_max(&st->last_active, static_cast<unsigned long long>(wall_clock64()), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();  // req is rewritten next round
   }
   if (threadIdx.x == 0 &&
       __hip_atomic_fetch_add(&st->exited, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) + 1 == gridDim.x)
@@ -906,8 +943,8 @@ __global__ __launch_bounds__(kBlock) void service_kernel(SvcCtl* ctl, SvcDev* st
 hipError_t launch_service(SvcCtl* d_ctl, SvcDev* d_state, unsigned long long epoch, unsigned long long idle_ticks,
                           unsigned long long life_ticks, hipStream_t s) {
   (void)hipGetLastError();
-  hipLaunchKernelGGL(service_kernel, dim3(kSvcSlots), dim3(kBlock), kSvcLds + 128, s, d_ctl, d_state, epoch,
-                     idle_ticks, life_ticks);
+  hipLaunchKernelGGL(service_kernel, dim3(kSvcSlots * kSvcParts), dim3(kSvcWave), kSvcLds + 128, s, d_ctl, d_state,
+                     epoch, idle_ticks, life_ticks);
   return hipGetLastError();
 }
 
