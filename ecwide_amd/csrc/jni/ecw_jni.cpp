@@ -9,12 +9,12 @@
 //
 //  * the work runs on the MI355X (ecw_encode / ecw_decode / ... copy the
 //    direct ByteBuffers through HBM in column slices, ecwide.h);
-//  * local parities are the XOR of their group (ECW_LOCAL_XOR) — the
-//    reference writes zeros (NativeCodec.cc:181-186); ECWIDE_LOCAL_MODE=literal
-//    reproduces its files byte for byte;
-//  * xorIntemediate XORs on every call — the reference's process-wide static
-//    `flag` (NativeCodec.cc:287-292) makes the first call write zeros;
-//    ECWIDE_XORI_LITERAL=1 reproduces that;
+//  * by default every byte is the reference's, quirks included: local parities
+//    are written as zeros (its XOR table is built from an all-zero matrix,
+//    NativeCodec.cc:176-186) and the process's first xorIntemediate writes
+//    zeros (its static `flag`, NativeCodec.cc:287-292). ECWIDE_LOCAL_MODE=xor
+//    writes the group XOR the design intends (what CL repair needs), and
+//    ECWIDE_XORI_LITERAL=0 XORs on every call;
 //  * errors the reference never checked (short arrays, non-direct buffers,
 //    device failures) raise a Java exception instead of crashing the JVM.
 //
@@ -143,7 +143,7 @@ ecw_codec* codec_of(JNIEnv* e, jobject o, ecw_codec_info* info) {
   if (f.code_type == 'L' && node < 1)
     node = f.decode_data_num == f.group_data_num ? 1 : (f.group_data_num - 1) * f.group_data_num + 1;
   const char* lm = std::getenv("ECWIDE_LOCAL_MODE");
-  const int local_mode = lm && std::strcmp(lm, "literal") == 0 ? ECW_LOCAL_LITERAL : ECW_LOCAL_XOR;
+  const int local_mode = lm && std::strcmp(lm, "xor") == 0 ? ECW_LOCAL_XOR : ECW_LOCAL_LITERAL;
   const Key key{f.code_type, k, f.global_num, r, node, f.multinode ? 1 : 0, local_mode, f.chunk_size};
   ecw_codec* cd = nullptr;
   {
@@ -306,7 +306,7 @@ JNIEXPORT void JNICALL Java_NativeCodec_xorIntemediate(JNIEnv* e, jobject o, job
     return;
   const char* lit = std::getenv("ECWIDE_XORI_LITERAL");
   const bool first = !g_xori_called.exchange(true);
-  if (first && lit && std::strcmp(lit, "1") == 0) {
+  if (first && !(lit && std::strcmp(lit, "0") == 0)) {
     // the reference's first call in the process runs with an all-zero table
     for (uint8_t* dst : t) std::memset(dst, 0, in.chunk_size);
     return;

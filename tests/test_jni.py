@@ -195,16 +195,17 @@ def test_errors_raise_java_exceptions(jni, manifest):
 
 @pytest.mark.gpu
 def test_xori_literal_first_call(jni, orc, manifest, monkeypatch):
-    """ECWIDE_XORI_LITERAL=1: the process's first xorIntemediate writes zeros, the
-    next ones XOR (NativeCodec.cc:284-323, static `flag`). Must be the first
-    xorIntemediate through this library in the process (it is: file order)."""
+    """The default (as ECWIDE_XORI_LITERAL unset): the process's first
+    xorIntemediate writes zeros, the next ones XOR (NativeCodec.cc:284-323,
+    static `flag`). Must be the first xorIntemediate through this library in
+    the process (it is: file order)."""
     e = manifest["xor_intermediate"]
     m, ln = e["m"], e["len"]
     s1, s2, s3 = e["seeds"]
     src1 = [orc.fill(ln, s1, 0, j) for j in range(m)]
     tgt = [orc.fill(ln, s2, 0, j) for j in range(m)]
     src2 = [orc.fill(ln, s3, 0, j) for j in range(m)]
-    monkeypatch.setenv("ECWIDE_XORI_LITERAL", "1")
+    monkeypatch.delenv("ECWIDE_XORI_LITERAL", raising=False)
     c = JavaCodec(jni, oracle_fields(orc, 8, m, 4, ln, 1), ln)
     assert c.xori(src1, tgt) == ""
     assert [sha(x) for x in tgt] == e["first"]
@@ -215,21 +216,23 @@ def test_xori_literal_first_call(jni, orc, manifest, monkeypatch):
 
 @pytest.mark.gpu
 def test_encode_golden_both_local_modes(jni, orc, manifest, monkeypatch):
+    """Default: ECWide-C's own bytes (zero L blocks); ECWIDE_LOCAL_MODE=xor:
+    the group XOR."""
     for e in manifest["encode"]:
         f, B = e["fields"], e["len"]
         data = [orc.fill(B, e["seed"], 0, j) for j in range(e["k"])]
         monkeypatch.delenv("ECWIDE_LOCAL_MODE", raising=False)
         c = JavaCodec(jni, f, B)
-        par = [np.full(B, 0x5A, np.uint8) for _ in range(c.parity_num)]
+        par = [np.full(B, 0xAB, np.uint8) for _ in range(c.parity_num)]
         assert c.encode(data, par) == "", e["name"]
-        want = golden_blocks(e["xor"], c.parity_num, B)
-        assert all(np.array_equal(g, w) for g, w in zip(par, want)), e["name"]
-        if e["code_type"] in "CL":
-            monkeypatch.setenv("ECWIDE_LOCAL_MODE", "literal")
-            c2 = JavaCodec(jni, f, B)
-            par2 = [np.full(B, 0xAB, np.uint8) for _ in range(c2.parity_num)]
-            assert c2.encode(data, par2) == ""
-            assert [sha(x) for x in par2] == e["literal_sha256"], e["name"]
+        lit = e["literal_sha256"] if e["code_type"] in "CL" else [sha(x) for x in golden_blocks(e["xor"], c.parity_num, B)]
+        assert [sha(x) for x in par] == lit, e["name"]
+        monkeypatch.setenv("ECWIDE_LOCAL_MODE", "xor")
+        c2 = JavaCodec(jni, f, B)
+        par2 = [np.full(B, 0x5A, np.uint8) for _ in range(c2.parity_num)]
+        assert c2.encode(data, par2) == ""
+        want = golden_blocks(e["xor"], c2.parity_num, B)
+        assert all(np.array_equal(g, w) for g, w in zip(par2, want)), e["name"]
 
 
 @pytest.mark.gpu
@@ -255,6 +258,8 @@ def test_multinode_chain_equals_single_node(jni, orc, monkeypatch):
     k, m, r, B = 20, 3, 6, 8192
     g = -(-k // r)
     monkeypatch.setenv("ECWIDE_K", str(k))
+    monkeypatch.setenv("ECWIDE_LOCAL_MODE", "xor")
+    monkeypatch.setenv("ECWIDE_XORI_LITERAL", "0")
     data = [orc.fill(B, 70, 0, j) for j in range(k)]
     single = JavaCodec(jni, oracle_fields(orc, k, m, r, B, 1), B)
     want = [np.zeros(B, np.uint8) for _ in range(single.parity_num)]
