@@ -1073,6 +1073,9 @@ struct Service {
 std::mutex g_mu;
 std::map<int, Service*> g_services;  // one per device, kept for the life of the process
 
+#ifndef ECW_SVC_SKEW
+#define ECW_SVC_SKEW 0  // bytes added to the staged block stride (tuning)
+#endif
 #ifndef ECW_SVC_TRACE
 #define ECW_SVC_TRACE 0  // tools only (tools/variants.py): per-phase latency of served calls, printed at exit
 #endif
@@ -1123,7 +1126,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     if (c->ensure_device() != ECW_OK) return kNotServed;  // the launch path reports the error
   }
   Service* sv = service_for(c->device);
-  const size_t cs = (len + 255) & ~static_cast<size_t>(255);
+  const size_t cs = ((len + 255) & ~static_cast<size_t>(255)) + ECW_SVC_SKEW;
   int slot;
   {
     std::unique_lock<std::mutex> lk(sv->mu);

@@ -144,7 +144,10 @@ int device_cu_count(int device);
 // once NO slot has had a request for `idle_ticks` of wall clock, or after
 // `life_ticks`; the last one out publishes exited_epoch = epoch, and the host
 // launches the next epoch when a request finds the service gone.
-constexpr int kSvcSlots = 16;  // concurrent callers served at once (one workgroup each)
+#ifndef ECW_SVC_SLOTS
+#define ECW_SVC_SLOTS 16
+#endif
+constexpr int kSvcSlots = ECW_SVC_SLOTS;  // concurrent callers served at once
 constexpr size_t kSvcMaxLen = size_t(64) << 10;   // bytes per block served (larger: launch path)
 constexpr size_t kSvcLds = size_t(60) << 10;       // LDS for the packed tables: k * 128 * nw bytes
 
@@ -185,6 +188,11 @@ struct SvcCtl {
 #endif
 constexpr int kSvcParts = ECW_SVC_PARTS;
 constexpr int kSvcWave = 64;  // threads per service workgroup (one wave)
+#ifndef ECW_SVC_UNIT
+#define ECW_SVC_UNIT 1024
+#endif
+constexpr uint32_t kSvcUnit = ECW_SVC_UNIT;  // column unit dealt to the parts (256, 512 or 1024 B)
+static_assert(kSvcUnit % 256 == 0 && kSvcUnit <= 1024 && 1024 % kSvcUnit == 0, "a unit is 16-64 lanes x 16 B");
 struct SvcDev {
   unsigned long long last_active;  // wall clock of the latest request served by any workgroup
   unsigned int exited;             // workgroups that left the loop

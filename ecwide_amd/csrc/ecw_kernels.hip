@@ -802,17 +802,25 @@ __device__ __forceinline__ void svc_columns(const SvcReq& q, uint32_t lds_base, 
   for (int l = 0; l < q.nrows; ++l) st16<true>(q.out + static_cast<uint64_t>(l) * q.cs, col, len, unpack_row<NW>(acc, l));
 }
 
-// this workgroup's column chunks (1 KiB: 64 lanes x 16 B) of a request
+// This part's column units of a request. A unit is kSvcUnit bytes (16 B per
+// lane); units are dealt round-robin over the parts, and the wave's lane
+// groups take kSvcGroups units at once: unit (s * kSvcGroups + group) *
+// kSvcParts + part in step s. Small blocks thus spread over many parts (one
+// wave reads pinned host memory at ~2 GB/s, so the bytes per part set the
+// call's load time).
 template <int NW, int LOCAL>
 __device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base, int part) {
-  constexpr uint32_t kChunk = kSvcWave * kLaneBytes;
-  for (unsigned long long c0 = static_cast<unsigned long long>(part) * kChunk; c0 < q.len;
-       c0 += static_cast<unsigned long long>(kSvcParts) * kChunk) {
-    const uint32_t col = static_cast<uint32_t>(c0) + threadIdx.x * kLaneBytes;
-    if (static_cast<unsigned long long>(col) + kLaneBytes <= q.len)
-      svc_columns<NW, LOCAL, false>(q, lds_base, col);
+  constexpr uint32_t kLanesPerUnit = kSvcUnit / kLaneBytes;
+  constexpr uint32_t kSvcGroups = kSvcWave / kLanesPerUnit;
+  const uint32_t grp = threadIdx.x / kLanesPerUnit, lane = threadIdx.x % kLanesPerUnit;
+  const unsigned long long step = static_cast<unsigned long long>(kSvcGroups) * kSvcParts * kSvcUnit;
+  // the step's first unit (group 0) decides for the whole wave
+  for (unsigned long long u0 = static_cast<unsigned long long>(part) * kSvcUnit; u0 < q.len; u0 += step) {
+    const unsigned long long col = u0 + static_cast<unsigned long long>(grp) * kSvcParts * kSvcUnit + lane * kLaneBytes;
+    if (col + kLaneBytes <= q.len)
+      svc_columns<NW, LOCAL, false>(q, lds_base, static_cast<uint32_t>(col));
     else if (col < q.len)
-      svc_columns<NW, LOCAL, true>(q, lds_base, col);
+      svc_columns<NW, LOCAL, true>(q, lds_base, static_cast<uint32_t>(col));
   }
 }
 
@@ -841,6 +849,16 @@ __device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base, 
 // (the host relaunches on exited_epoch), which serves it whole. A request's tables stay staged in LDS
 // while the next request uses the same codec (same table address).
 constexpr unsigned long long kSvcLeave = ~0ull;  // SvcDev::Slot::seq: part 0 has left
+#ifndef ECW_SVC_ACQ
+#define ECW_SVC_ACQ 1  // tuning only: 0 drops the acquire fence after a request is seen
+#endif
+#ifndef ECW_SVC_POLL_SLEEP
+#define ECW_SVC_POLL_SLEEP 0
+#endif
+#ifndef ECW_SVC_POLL_DEPTH
+#define ECW_SVC_POLL_DEPTH 1
+#endif
+constexpr int kSvcPollDepth = ECW_SVC_POLL_DEPTH;
 
 __global__ __launch_bounds__(kSvcWave) void service_kernel(SvcCtl* ctl, SvcDev* st, unsigned long long epoch,
                                                            unsigned long long idle_ticks,
@@ -865,9 +883,29 @@ __global__ __launch_bounds__(kSvcWave) void service_kernel(SvcCtl* ctl, SvcDev* 
     // (the whole wave loads the same word: uniform control flow) ---
     unsigned long long seq = 0;
     bool leave = false;
+    // kSvcPollDepth polls in flight: a new one is issued as each returns, so a
+    // posted request is seen about one PCIe read latency after it lands, not
+    // up to two
+    unsigned long long inflight[kSvcPollDepth];
+#pragma unroll
+    for (int i = 0; i < kSvcPollDepth; ++i) inflight[i] = sys_load_relaxed(&slot->seq);
     for (int spin = 1;; ++spin) {
-      seq = sys_load_relaxed(&slot->seq);
-      if (seq != last) break;
+      bool seen = false;
+#pragma unroll
+      for (int i = 0; i < kSvcPollDepth; ++i) {
+        // the oldest poll: wait for it alone, reissue it, then look at it
+        const unsigned long long v = inflight[i];
+        inflight[i] = sys_load_relaxed(&slot->seq);
+        if (v != last) {
+          seq = v;
+          seen = true;
+          break;
+        }
+      }
+      if (seen) break;
+#if ECW_SVC_POLL_SLEEP
+      __builtin_amdgcn_s_sleep(ECW_SVC_POLL_SLEEP);  // tuning: fewer PCIe reads while idle
+#endif
       if ((spin & 63) == 0) {
         // part 0 decides for its slot (idle, lifetime, stop) and tells the other
         // parts through device memory; they watch that, the stop flag and the
@@ -894,7 +932,12 @@ __global__ __launch_bounds__(kSvcWave) void service_kernel(SvcCtl* ctl, SvcDev* 
     if (part == 0 && threadIdx.x == 0)
       __hip_atomic_fetch_max(&st->last_active, static_cast<unsigned long long>(wall_clock64()), __ATOMIC_RELAXED,
                              __HIP_MEMORY_SCOPE_AGENT);
+#if ECW_SVC_ACQ
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // system scope: the request and its blocks are visible
+#endif
+#if ECW_SVC_TRACE
+    trace[1] = static_cast<unsigned long long>(wall_clock64());
+#endif
     const unsigned long long gen = seq >> kSvcSeqBits;
     if (gen != req_gen) {  // new request words: 9 lanes read them at once
       if (threadIdx.x < kSvcReqWords)
@@ -911,6 +954,9 @@ __global__ __launch_bounds__(kSvcWave) void service_kernel(SvcCtl* ctl, SvcDev* 
       staged_n16 = n16;
       __syncthreads();
     }
+#if ECW_SVC_TRACE
+    trace[2] = static_cast<unsigned long long>(wall_clock64());
+#endif
     if (q.nw == 2)
       svc_request<2>(q, lds_base, part);
     else

@@ -45,12 +45,35 @@ def main():
     pp = (ctypes.c_void_p * m)(*[x.ctypes.data for x in p])
     for _ in range(100):
         assert L.ecw_encode(h, dp, pp, ln) == 0
+    nt = int(os.environ.get("THREADS", 1))
+    name = os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else "libecwide.so"
+    if nt == 1:
+        t = time.perf_counter()
+        for _ in range(n):
+            L.ecw_encode(h, dp, pp, ln)
+        el = time.perf_counter() - t
+        print(f"{name}: {el / n * 1e6:.2f} us per synchronous k={k} m={m} {ln} B call "
+              f"({(k + m) * ln * n / el / 1e9:.2f} GB/s)", flush=True)
+        return
+    import threading
+
+    def worker():  # each thread its own buffers; ctypes drops the GIL in the call
+        d2 = [x.copy() for x in d]
+        p2 = [np.zeros(ln, np.uint8) for _ in range(m)]
+        a = (ctypes.c_void_p * k)(*[x.ctypes.data for x in d2])
+        b = (ctypes.c_void_p * m)(*[x.ctypes.data for x in p2])
+        for _ in range(n):
+            L.ecw_encode(h, a, b, ln)
+
+    th = [threading.Thread(target=worker) for _ in range(nt)]
     t = time.perf_counter()
-    for _ in range(n):
-        L.ecw_encode(h, dp, pp, ln)
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
     el = time.perf_counter() - t
-    print(f"{os.path.basename(sys.argv[1]) if len(sys.argv) > 1 else 'libecwide.so'}: {el / n * 1e6:.2f} us per "
-          f"synchronous k={k} m={m} {ln} B call", flush=True)
+    print(f"{name}: {nt} threads x {n} synchronous k={k} m={m} {ln} B calls: "
+          f"{(k + m) * ln * n * nt / el / 1e9:.2f} GB/s", flush=True)
 
 
 if __name__ == "__main__":
