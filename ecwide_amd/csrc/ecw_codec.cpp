@@ -1073,15 +1073,12 @@ struct Service {
 std::mutex g_mu;
 std::map<int, Service*> g_services;  // one per device, kept for the life of the process
 
-#ifndef ECW_SVC_SKEW
-#define ECW_SVC_SKEW 0  // bytes added to the staged block stride (tuning)
-#endif
 #ifndef ECW_SVC_TRACE
 #define ECW_SVC_TRACE 0  // tools only (tools/variants.py): per-phase latency of served calls, printed at exit
 #endif
 #if ECW_SVC_TRACE
-// host ns: copy in, post -> done seen, copy out; device ticks: detect -> words,
-// words -> start, start -> computed, computed -> fenced
+// host ns: copy in, post -> done seen, copy out; device ticks of the last
+// part: seen -> acquired, -> start, -> computed, -> fenced
 double g_tr[7] = {};
 unsigned long long g_tr_n = 0;
 #endif
@@ -1095,8 +1092,8 @@ void stop_all() {
     (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
     const double n = static_cast<double>(g_tr_n), tick_us = 1e3 / khz;
     std::fprintf(stderr,
-                 "svc trace (%llu calls, us): copy-in %.2f  post->done %.2f  copy-out %.2f | device: part 0 saw it -> "
-                 "the last part saw it %.2f  -> start %.2f  -> computed %.2f  -> fenced %.2f\n",
+                 "svc trace (%llu calls, us): copy-in %.2f  post->done %.2f  copy-out %.2f | device (last part): seen -> "
+                 "acquired %.2f  -> start %.2f  -> computed %.2f  -> fenced %.2f\n",
                  g_tr_n, g_tr[0] / n / 1e3, g_tr[1] / n / 1e3, g_tr[2] / n / 1e3, g_tr[3] / n * tick_us,
                  g_tr[4] / n * tick_us, g_tr[5] / n * tick_us, g_tr[6] / n * tick_us);
   }
@@ -1126,7 +1123,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     if (c->ensure_device() != ECW_OK) return kNotServed;  // the launch path reports the error
   }
   Service* sv = service_for(c->device);
-  const size_t cs = ((len + 255) & ~static_cast<size_t>(255)) + ECW_SVC_SKEW;
+  const size_t cs = (len + 255) & ~static_cast<size_t>(255);
   int slot;
   {
     std::unique_lock<std::mutex> lk(sv->mu);
@@ -1178,14 +1175,16 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     w.nw = nw;
     return w;
   }();
-  constexpr unsigned long long kSeqMask = (1ull << kSvcSeqBits) - 1;
   unsigned long long gen = q.seq >> kSvcSeqBits;
   const size_t words = offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl);
   if (q.seq == 0 || std::memcmp(&want.tbl, &q.tbl, words) != 0) {  // new request words: a new generation
     std::memcpy(&q.tbl, &want.tbl, words);
     gen = (gen + 1) & ((1ull << (64 - kSvcSeqBits)) - 1);
   }
-  const unsigned long long seq = (gen << kSvcSeqBits) | (((q.seq & kSeqMask) + 1) & kSeqMask);
+  const unsigned long long units = (len + kSvcThreads * 4 - 1) / (kSvcThreads * 4);
+  const int active = static_cast<int>(std::min<unsigned long long>(units, kSvcParts));
+  const unsigned long long seq = (gen << kSvcSeqBits) | (static_cast<unsigned long long>(active) << 32) |
+                                 (((q.seq & kSvcReqMask) + 1) & kSvcReqMask);
   __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
   bool up;
   {
@@ -1196,13 +1195,19 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
   if (!up) return release(kNotServed);
   const auto t0 = std::chrono::steady_clock::now();
   int failed = ECW_OK;
-  for (unsigned spins = 1; __atomic_load_n(&q.done, __ATOMIC_ACQUIRE) != seq; ++spins) {
+  // every part with work publishes its own done word (one cache line)
+  auto finished = [&] {
+    for (int p = 0; p < active; ++p)
+      if (__atomic_load_n(&q.done[p], __ATOMIC_ACQUIRE) != seq) return false;
+    return true;
+  };
+  for (unsigned spins = 1; !finished(); ++spins) {
     if (spins % 1024) {
       __builtin_ia32_pause();
       continue;
     }
     std::lock_guard<std::mutex> lk(sv->mu);
-    if (__atomic_load_n(&q.done, __ATOMIC_ACQUIRE) == seq) break;
+    if (finished()) break;
     // the epoch this request was posted to left before serving it: start the next one
     if (sv->ensure_running() != ECW_OK ||
         std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {  // 10 s: the device is gone
@@ -1224,7 +1229,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     g_tr[0] += ns(tr1 - tr0);
     g_tr[1] += ns(tr2 - tr1);
     g_tr[2] += ns(tr3 - tr2);
-    for (int i = 0; i < 4; ++i) g_tr[3 + i] += static_cast<double>(q.pad1[i + 1] - q.pad1[i]);
+    for (int i = 0; i < 4; ++i) g_tr[3 + i] += static_cast<double>(q.trace[i + 1] - q.trace[i]);
     ++g_tr_n;
   }
 #endif

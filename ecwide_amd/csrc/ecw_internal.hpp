@@ -151,23 +151,43 @@ constexpr int kSvcSlots = ECW_SVC_SLOTS;  // concurrent callers served at once
 constexpr size_t kSvcMaxLen = size_t(64) << 10;   // bytes per block served (larger: launch path)
 constexpr size_t kSvcLds = size_t(60) << 10;       // LDS for the packed tables: k * 128 * nw bytes
 
-// `seq` and `done` hold a request word: the request number in the low
-// kSvcSeqBits bits, the generation of the request words below in the bits
-// above. The host bumps the generation only when the request words change
-// (another codec, length or staging), so a workgroup that already holds that
-// generation skips reading them: one PCIe round trip less per call.
+// `seq` and `done` hold a request word: the request number in the low 32
+// bits, the number of parts with work (one per 1 KiB column unit, at most
+// kSvcParts) in bits 32..39, the generation of the request words below in the
+// bits from kSvcSeqBits. The host bumps the generation only when the request
+// words change (another codec, length or staging), so a workgroup that
+// already holds that generation skips reading them: one PCIe round trip less
+// per call. Parts without work only note the word; the host waits for the
+// others' done words.
 constexpr int kSvcSeqBits = 40;
+constexpr unsigned long long kSvcReqMask = 0xFFFFFFFFull;
+__host__ __device__ inline int svc_active_parts(unsigned long long seq) { return static_cast<int>((seq >> 32) & 0xFF); }
+
+// Each slot is served by kSvcParts workgroups of kSvcThreads lanes, each
+// taking every kSvcParts-th 1 KiB column unit (one dword per lane): the
+// blocks of a call come in through several CUs at once (one wave reads pinned
+// host memory at ~2 GB/s) and its GF products run on four SIMDs per part.
+// Wave 0 of every part polls the slot; every part publishes its own `done`
+// word, and the call is finished when all of them hold its request word.
+#ifndef ECW_SVC_PARTS
+#define ECW_SVC_PARTS 8
+#endif
+constexpr int kSvcParts = ECW_SVC_PARTS;
+static_assert(kSvcParts >= 1 && kSvcParts <= 8, "one done word per part in the slot's second line");
+constexpr int kSvcWave = 64;       // wave size
+constexpr int kSvcThreads = 256;   // threads per service workgroup (four waves)
+
 struct alignas(64) SvcSlot {
   unsigned long long seq;    // host: word of the latest request
   unsigned long long pad0[7];
-  unsigned long long done;   // device: word of the latest finished request
-  unsigned long long pad1[7];
+  unsigned long long done[8];  // device: word of the latest request part p finished
   // the request words (written by the host before `seq` when they change)
   const void* tbl;           // packed tables of the codec's pass 0 (device memory)
   uint8_t* data;             // k input rows, `cs` bytes apart (device view of pinned staging)
   uint8_t* out;              // parity rows [G.., L..], `cs` bytes apart
   unsigned long long len, cs;
   int k, nrows, m, r, groups, local_mode, nw, pad2;
+  unsigned long long trace[8];  // tools only (ECW_SVC_TRACE): phase stamps of the last part
 };
 
 struct SvcCtl {
@@ -178,29 +198,13 @@ struct SvcCtl {
 };
 
 // device-memory state of one service launch (zeroed before every launch)
-// Each slot is served by kSvcParts single-wave workgroups, each taking every
-// kSvcParts-th 1 KiB column chunk: one wave reads pinned host memory at ~2 GB/s
-// (a 4 KiB k=11 call: 20.5 us of loads with 1 part, 2.8 us with 8), so a call's
-// blocks come in through 8 waves at once. Every part polls the slot; the last
-// part to finish publishes `done`.
-#ifndef ECW_SVC_PARTS
-#define ECW_SVC_PARTS 8
-#endif
-constexpr int kSvcParts = ECW_SVC_PARTS;
-constexpr int kSvcWave = 64;  // threads per service workgroup (one wave)
-#ifndef ECW_SVC_UNIT
-#define ECW_SVC_UNIT 1024
-#endif
-constexpr uint32_t kSvcUnit = ECW_SVC_UNIT;  // column unit dealt to the parts (256, 512 or 1024 B)
-static_assert(kSvcUnit % 256 == 0 && kSvcUnit <= 1024 && 1024 % kSvcUnit == 0, "a unit is 16-64 lanes x 16 B");
 struct SvcDev {
   unsigned long long last_active;  // wall clock of the latest request served by any workgroup
   unsigned int exited;             // workgroups that left the loop
   unsigned int pad;
   struct Slot {
     unsigned long long seq;        // kSvcLeave once part 0 has left (tells the other parts)
-    unsigned int fin;              // parts finished (monotonic; the one that makes it a multiple of kSvcParts publishes)
-    unsigned int pad[13];
+    unsigned long long pad[7];
   } slot[kSvcSlots];
 };
 

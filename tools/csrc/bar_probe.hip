@@ -42,11 +42,19 @@ __global__ void echo(const unsigned long long* flag, unsigned long long* ack, in
 // bytes apart) from pinned host memory, cache-bypassing, all in flight at
 // once; wall-clock ticks from issue to the last return, `iters` times
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-__global__ void fetch(const uint8_t* src, size_t stride, int rows, int iters, unsigned long long* ticks) {
-  unsigned long long total = 0;
+// fence = 1: a system-scope acquire before each fetch (what the service
+// does after seeing a request), so the rows come over PCIe, not from L2;
+// ticks[2] accumulates the fence's own time
+__global__ void fetch(const uint8_t* src, size_t stride, int rows, int iters, unsigned long long* ticks, int fence) {
+  unsigned long long total = 0, ftot = 0;
   uint32_t sink = 0;
   for (int it = 0; it < iters; ++it) {
     const uint8_t* base = src + static_cast<size_t>(it % 16) * stride * 16;
+    if (fence) {
+      const unsigned long long f0 = wall_clock64();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      ftot += wall_clock64() - f0;
+    }
     const unsigned long long t0 = wall_clock64();
     u32x4 v[16];
 #pragma unroll
@@ -58,7 +66,51 @@ __global__ void fetch(const uint8_t* src, size_t stride, int rows, int iters, un
     __builtin_amdgcn_s_waitcnt(0);
     total += wall_clock64() - t0;
   }
-  if (threadIdx.x == 0) ticks[0] = total;
+  if (threadIdx.x == 0) {
+    ticks[0] = total;
+    ticks[2] = ftot;
+  }
+  if (sink == 0x12345678u) ticks[1] = sink;
+}
+
+// the service's own access: volatile raw buffer loads (sc0 sc1), `waves`
+// workgroups at once each on its own 1 KiB column, after a system acquire;
+// then (stores = 1) 3 buffer stores of 1 KiB back and a wait for them
+__global__ void fetch_svc(uint8_t* src, size_t stride, int rows, int iters, unsigned long long* ticks, int stores) {
+  unsigned long long total = 0, stot = 0;
+  uint32_t sink = 0;
+  for (int it = 0; it < iters; ++it) {
+    uint8_t* base = src + static_cast<size_t>(it % 16) * stride * 16 + blockIdx.x * 1024;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    const unsigned long long t0 = wall_clock64();
+    u32x4 v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r < rows) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + r * stride, 0, 0x7FFFFFFF, 0x00020000);
+        v[r] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(threadIdx.x * 16), 0, static_cast<int>(0x80000000u));
+      }
+    u32x4 acc = {0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r < rows) acc ^= v[r];
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t1 = wall_clock64();
+    total += t1 - t0;
+    if (stores) {
+      for (int l = 0; l < 3; ++l) {
+        const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(base + (12 + l) * stride, 0, 0x7FFFFFFF, 0x00020000);
+        __builtin_amdgcn_raw_buffer_store_b128(acc + static_cast<unsigned>(l), rs, static_cast<int>(threadIdx.x * 16), 0, 0);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      stot += wall_clock64() - t1;
+    }
+    sink ^= acc.x;
+  }
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    ticks[0] = total;
+    ticks[2] = stot;
+  }
   if (sink == 0x12345678u) ticks[1] = sink;
 }
 
@@ -106,16 +158,42 @@ int main() {
     void* dhs = nullptr;
     CK(hipHostGetDevicePointer(&dhs, hs, 0));
     unsigned long long* tk = nullptr;
-    CK(hipMalloc(reinterpret_cast<void**>(&tk), 16));
-    for (int rows : {1, 4, 11, 16}) {
-      const int iters = 2000;
-      hipLaunchKernelGGL(fetch, dim3(1), dim3(64), 0, 0, static_cast<const uint8_t*>(dhs), stride, rows, iters, tk);
-      CK(hipGetLastError());
-      unsigned long long t = 0;
-      CK(hipMemcpy(&t, tk, 8, hipMemcpyDeviceToHost));
-      std::printf("one wave, %2d x 1 KiB rows from pinned host memory: %.2f us per fetch\n", rows,
-                  static_cast<double>(t) / iters * 1e3 / khz);
-    }
+    CK(hipMalloc(reinterpret_cast<void**>(&tk), 32));
+    for (int fence : {0, 1})
+      for (int rows : {1, 4, 11, 16}) {
+        const int iters = 2000;
+        hipLaunchKernelGGL(fetch, dim3(1), dim3(64), 0, 0, static_cast<const uint8_t*>(dhs), stride, rows, iters, tk,
+                           fence);
+        CK(hipGetLastError());
+        unsigned long long t[3] = {};
+        CK(hipMemcpy(t, tk, 24, hipMemcpyDeviceToHost));
+        std::printf("one wave, %2d x 1 KiB rows from pinned host memory, %s: %.2f us per fetch (fence %.2f us)\n", rows,
+                    fence ? "after a system acquire" : "no fence", static_cast<double>(t[0]) / iters * 1e3 / khz,
+                    static_cast<double>(t[2]) / iters * 1e3 / khz);
+      }
+  }
+  {
+    int khz = 0;
+    CK(hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0));
+    uint8_t* hs = nullptr;
+    const size_t stride = 4096;
+    CK(hipHostMalloc(reinterpret_cast<void**>(&hs), stride * 16 * 16, hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(hs, 1, stride * 16 * 16);
+    void* dhs = nullptr;
+    CK(hipHostGetDevicePointer(&dhs, hs, 0));
+    unsigned long long* tk = nullptr;
+    CK(hipMalloc(reinterpret_cast<void**>(&tk), 32));
+    for (int stores : {0, 1})
+      for (int waves : {1, 4}) {
+        const int iters = 2000, rows = 11;
+        hipLaunchKernelGGL(fetch_svc, dim3(waves), dim3(64), 0, 0, static_cast<uint8_t*>(dhs), stride, rows, iters, tk,
+                           stores);
+        CK(hipGetLastError());
+        unsigned long long t[3] = {};
+        CK(hipMemcpy(t, tk, 24, hipMemcpyDeviceToHost));
+        std::printf("service access, %d wave(s), 11 x 1 KiB volatile buffer loads: %.2f us per fetch; 3 stores + release: %.2f us\n",
+                    waves, static_cast<double>(t[0]) / iters * 1e3 / khz, static_cast<double>(t[2]) / iters * 1e3 / khz);
+      }
   }
   void* d = nullptr;
   CK(hipExtMallocWithFlags(&d, 1 << 20, hipDeviceMallocFinegrained));
