@@ -110,3 +110,20 @@ def test_service_then_device_sync_and_clean_exit(E, orc):
             "c.encodeData(d, p); print('ok', int(p[0].sum()))\n") % REPO
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0 and p.stdout.startswith("ok"), p.stderr[-2000:]
+
+
+def test_service_alternating_shapes_one_slot(E, orc):
+    """One thread (one slot) alternating codecs and lengths call after call:
+    the request words change generation every call, and the number of parts
+    with work swings between 1 and 8, so parts that sat out a request (and may
+    not have seen it yet) must take the next one whole."""
+    rs = (E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 65536)), orc.codec("R", 11, 3, 11, 65536))
+    cl = (E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(24, 2, 5, 65536), 1, False),
+          orc.codec("C", 24, 2, 5, 65536))
+    for n, ln in enumerate([65536, 1, 40000, 17, 1024, 65536, 3 * 1024 + 5, 1, 65536]):
+        for c, oc in (rs, cl):
+            data = [orc.fill(ln, 700 + n, 0, j) for j in range(c.encodeDataNum)]
+            par = [np.full(ln, 0x3C, np.uint8) for _ in range(c.parityNum)]
+            c.encodeData(data, par)
+            for i, w in enumerate(oc.encode(data)):
+                assert np.array_equal(par[i], w[:ln]), (n, ln, i)
