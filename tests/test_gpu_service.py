@@ -127,3 +127,25 @@ def test_service_alternating_shapes_one_slot(E, orc):
             c.encodeData(data, par)
             for i, w in enumerate(oc.encode(data)):
                 assert np.array_equal(par[i], w[:ln]), (n, ln, i)
+
+
+def test_service_exit_after_every_request(E):
+    """ECW_SERVICE_IDLE_MS=0: the resident kernel leaves at its first idle
+    check after every request, so calls keep racing its exit and relaunch
+    (a request posted while the epoch leaves is served by the next one).
+    Runs in a child process (the setting is read once per process)."""
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "import numpy as np, ecwide_amd as E, oracle\n"
+            "orc = oracle.Oracle()\n"
+            "c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 8192))\n"
+            "oc = orc.codec('R', 11, 3, 11, 8192)\n"
+            "for n in range(300):\n"
+            "    ln = (4096, 8192, 100)[n %% 3]\n"
+            "    d = [orc.fill(ln, 50 + n, 0, j) for j in range(11)]\n"
+            "    p = [np.zeros(ln, np.uint8) for _ in range(3)]\n"
+            "    c.encodeData(d, p)\n"
+            "    assert all(np.array_equal(a, b) for a, b in zip(p, oc.encode(d))), n\n"
+            "print('ok')\n") % REPO
+    env = dict(os.environ, ECW_SERVICE_IDLE_MS="0")
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
+    assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
