@@ -42,7 +42,7 @@ TICKET_MIN_TILES = 4 * ENCODE_LAUNCH_TILES  # ECW_TICKET_MIN_TILES: one ticket-o
 class StripeSlab:
     def __init__(self, codec: NativeCodec, stripes: int, block_bytes: int | None = None,
                  pad: int = DEFAULT_PAD, device: int | None = None, layout: str = "blocks",
-                 chunk: int = DEFAULT_CHUNK, unit_pad: int = 0):
+                 chunk: int = DEFAULT_CHUNK, unit_pad: int = 0, base_offset: int = 0):
         import torch
 
         self.codec = codec
@@ -77,8 +77,11 @@ class StripeSlab:
             nbytes = self.parity_offset + self.units * self.punit_stride
         else:
             raise ValueError(f"unknown layout {layout!r}")
-        self.buf = torch.empty(nbytes, dtype=torch.uint8, device=f"cuda:{dev}")
-        self.base = self.buf.data_ptr()
+        if base_offset % 256 or base_offset < 0:
+            raise ValueError("base_offset must be a non-negative multiple of 256")
+        self.off = base_offset  # where the slab starts inside its allocation
+        self.buf = torch.empty(nbytes + base_offset, dtype=torch.uint8, device=f"cuda:{dev}")
+        self.base = self.buf.data_ptr() + base_offset
 
     def _split_args(self):
         if self.layout == "split":
@@ -93,19 +96,19 @@ class StripeSlab:
     def block(self, s: int, b: int):
         """Block b of stripe s (a view; in the tiled layout a contiguous copy)."""
         if self.layout == "blocks":
-            o = s * self.stripe_stride + b * self.block_stride
+            o = self.off + s * self.stripe_stride + b * self.block_stride
             return self.buf[o:o + self.len]
         k, np_ = self.codec.encodeDataNum, self.codec.parityNum
         if self.layout == "split":
-            o = (s * self.stripe_stride + b * self.block_stride if b < k else
-                 self.parity_offset + s * self.pstripe_stride + (b - k) * self.block_stride)
+            o = self.off + (s * self.stripe_stride + b * self.block_stride if b < k else
+                            self.parity_offset + s * self.pstripe_stride + (b - k) * self.block_stride)
             return self.buf[o:o + self.len]
         ch = self.chunk
         if b < k:
             o, step = s * self.pieces * self.unit_stride + b * ch, self.unit_stride
         else:
             o, step = self.parity_offset + s * self.pieces * self.punit_stride + (b - k) * ch, self.punit_stride
-        return self.buf.as_strided((self.pieces, ch), (step, 1), o).reshape(-1)
+        return self.buf.as_strided((self.pieces, ch), (step, 1), self.off + o).reshape(-1)
 
     def data(self, s: int):
         return [self.block(s, j) for j in range(self.codec.encodeDataNum)]

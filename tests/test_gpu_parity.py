@@ -275,7 +275,7 @@ def test_ticket_launch_matches_windows(E, torch, orc, k, m, r, B, S, layout, loc
         for i, w in enumerate(want):
             assert np.array_equal(pbuf[i][B - W:].cpu().numpy(), w), (s, i)
     if layout == "tiled":
-        slab.buf[slab.parity_offset:].zero_()
+        slab.buf[slab.off + slab.parity_offset:].zero_()
     else:
         for p in slab.parity(0) + slab.parity(S - 1):
             p.zero_()
