@@ -62,6 +62,7 @@ struct ecw_codec {
   std::vector<uint8_t> gftbl;         // 32 * edn * m (encodeGftbl, ISA-L layout)
   std::vector<uint8_t> dtbl, pdtbl;   // decode / partial-decode tables (all ones)
   std::vector<std::vector<uint8_t>> pass_img;  // packed device tables per pass of <= 8 rows
+  bool xor_row = false;               // m == 1 and every coefficient 1: the global parity is a plain XOR
 
   std::mutex mu;                      // guards everything below
   bool dev_ready = false;
@@ -533,6 +534,7 @@ int ecw_matrix_codec_create(const uint8_t* matrix, int k, int rows, int device, 
   in.group_data_num = -1;
   in.parity_num = rows;
   c->matrix.assign(matrix, matrix + static_cast<size_t>(k) * rows);
+  c->xor_row = rows == 1 && std::all_of(c->matrix.begin(), c->matrix.end(), [](uint8_t v) { return v == 1; });
   c->gftbl = isal_tables(k, rows, c->matrix.data());
   std::vector<uint8_t> ones(256, 1);
   c->dtbl = isal_tables(k, 1, ones.data());
@@ -1173,10 +1175,11 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     w.groups = c->groups();
     w.local_mode = local_mode_of(c);
     w.nw = nw;
+    w.flags = c->xor_row ? kSvcXorRow : 0;
     return w;
   }();
   unsigned long long gen = q.seq >> kSvcSeqBits;
-  const size_t words = offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl);
+  const size_t words = offsetof(SvcSlot, flags) + sizeof(int) - offsetof(SvcSlot, tbl);
   if (q.seq == 0 || std::memcmp(&want.tbl, &q.tbl, words) != 0) {  // new request words: a new generation
     std::memcpy(&q.tbl, &want.tbl, words);
     gen = (gen + 1) & ((1ull << (64 - kSvcSeqBits)) - 1);

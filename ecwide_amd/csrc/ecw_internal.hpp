@@ -160,6 +160,7 @@ constexpr size_t kSvcLds = size_t(60) << 10;       // LDS for the packed tables:
 // per call. Parts without work only note the word; the host waits for the
 // others' done words.
 constexpr int kSvcSeqBits = 40;
+constexpr int kSvcXorRow = 1;  // request flag: one global row, all coefficients 1 (a plain XOR)
 constexpr unsigned long long kSvcReqMask = 0xFFFFFFFFull;
 __host__ __device__ inline int svc_active_parts(unsigned long long seq) { return static_cast<int>((seq >> 32) & 0xFF); }
 
@@ -186,7 +187,7 @@ struct alignas(64) SvcSlot {
   uint8_t* data;             // k input rows, `cs` bytes apart (device view of pinned staging)
   uint8_t* out;              // parity rows [G.., L..], `cs` bytes apart
   unsigned long long len, cs;
-  int k, nrows, m, r, groups, local_mode, nw, pad2;
+  int k, nrows, m, r, groups, local_mode, nw, flags;  // flags: kSvcXorRow
   unsigned long long trace[8];  // tools only (ECW_SVC_TRACE): phase stamps of the last part
 };
 

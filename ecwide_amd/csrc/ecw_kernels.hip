@@ -758,11 +758,11 @@ struct SvcReq {
   uint8_t* data;
   uint8_t* out;
   unsigned long long len, cs;
-  int k, nrows, m, r, groups, local_mode, nw, pad;
+  int k, nrows, m, r, groups, local_mode, nw, flags;
 };
 constexpr int kSvcReqWords = 9;
 static_assert(sizeof(SvcReq) == 8 * kSvcReqWords, "SvcReq mirrors the request words of SvcSlot");
-static_assert(offsetof(SvcSlot, pad2) + sizeof(int) - offsetof(SvcSlot, tbl) == sizeof(SvcReq), "SvcSlot request layout");
+static_assert(offsetof(SvcSlot, flags) + sizeof(int) - offsetof(SvcSlot, tbl) == sizeof(SvcReq), "SvcSlot request layout");
 
 #ifndef ECW_SVC_ABLATE
 #define ECW_SVC_ABLATE 0  // tuning only: 1 leaves the GF products out of served requests
@@ -845,7 +845,7 @@ __device__ __forceinline__ uint32_t unpack_dw(const uint32_t (&acc)[4 * NW], int
 // One lane's dword of a served request. All input rows of a round of 16 are
 // loaded before the first product (one PCIe round trip per 16 rows). The
 // request's words are taken into registers first.
-template <int NW, int LOCAL, bool TAIL>
+template <int NW, int LOCAL, bool TAIL, bool XORROW>
 __device__ __forceinline__ void svc_dword(const SvcReq& q, uint32_t lds_base, uint32_t col) {
   const uint32_t len = static_cast<uint32_t>(q.len);
   const int k = q.k, r = q.r, m = q.m, nrows = q.nrows;
@@ -869,7 +869,10 @@ __device__ __forceinline__ void svc_dword(const SvcReq& q, uint32_t lds_base, ui
 #if ECW_SVC_ABLATE
       acc[0] ^= v[u];  // tuning only: the math left out
 #else
-      gf_dw<NW>(v[u], acc, lds_base + static_cast<uint32_t>(j) * (128u * NW));
+      if constexpr (XORROW)
+        acc[0] ^= v[u];  // coefficient 1 everywhere: the product is the byte itself
+      else
+        gf_dw<NW>(v[u], acc, lds_base + static_cast<uint32_t>(j) * (128u * NW));
 #endif
       if constexpr (LOCAL != kLocalNone) {
         lacc ^= v[u];
@@ -883,28 +886,36 @@ __device__ __forceinline__ void svc_dword(const SvcReq& q, uint32_t lds_base, ui
       }
     }
   }
-  for (int l = 0; l < nrows; ++l)
-    svc_st4<TAIL>(const_cast<uint8_t*>(uniform_ptr(out + static_cast<uint64_t>(l) * cs)), col, len, unpack_dw<NW>(acc, l));
+  if constexpr (XORROW) {
+    svc_st4<TAIL>(const_cast<uint8_t*>(uniform_ptr(out)), col, len, acc[0]);
+  } else {
+    for (int l = 0; l < nrows; ++l)
+      svc_st4<TAIL>(const_cast<uint8_t*>(uniform_ptr(out + static_cast<uint64_t>(l) * cs)), col, len,
+                    unpack_dw<NW>(acc, l));
+  }
 }
 
 // This part's column units of a request: units of kSvcThreads dwords dealt
 // round-robin over the parts.
-template <int NW, int LOCAL>
+template <int NW, int LOCAL, bool XORROW = false>
 __device__ __forceinline__ void svc_local(const SvcReq& q, uint32_t lds_base, int part) {
   constexpr uint32_t kUnit = kSvcThreads * 4;
   for (unsigned long long u0 = static_cast<unsigned long long>(part) * kUnit; u0 < q.len;
        u0 += static_cast<unsigned long long>(kSvcParts) * kUnit) {
     const unsigned long long col = u0 + threadIdx.x * 4u;
     if (col + 4 <= q.len)
-      svc_dword<NW, LOCAL, false>(q, lds_base, static_cast<uint32_t>(col));
+      svc_dword<NW, LOCAL, false, XORROW>(q, lds_base, static_cast<uint32_t>(col));
     else if (col < q.len)
-      svc_dword<NW, LOCAL, true>(q, lds_base, static_cast<uint32_t>(col));
+      svc_dword<NW, LOCAL, true, XORROW>(q, lds_base, static_cast<uint32_t>(col));
   }
 }
 
 template <int NW>
 __device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base, int part) {
-  if (q.local_mode == kLocalXor)
+  // ECWide-H's l_encode / l_middle / l_decode: one all-ones row, no locals
+  if (NW == 1 && (q.flags & kSvcXorRow) && q.local_mode == kLocalNone)
+    svc_local<1, kLocalNone, true>(q, lds_base, part);
+  else if (q.local_mode == kLocalXor)
     svc_local<NW, kLocalXor>(q, lds_base, part);
   else if (q.local_mode == kLocalZero)
     svc_local<NW, kLocalZero>(q, lds_base, part);

@@ -149,3 +149,28 @@ def test_service_exit_after_every_request(E):
     env = dict(os.environ, ECW_SERVICE_IDLE_MS="0")
     p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=180, env=env)
     assert p.returncode == 0 and p.stdout.strip().endswith("ok"), p.stderr[-2000:]
+
+
+@pytest.mark.parametrize("k", [11, 4, 5])
+def test_service_xor_row_matrix_codec(E, orc, k):
+    """ECWide-H's l_encode / l_middle / l_decode (k = 11 / 4 / 5): one all-ones
+    row through ecw_matrix_codec_create (as the ISA-L shim builds it) takes
+    the service's plain-XOR path; ragged and unit-straddling lengths."""
+    import ctypes
+
+    from ecwide_amd import _lib
+
+    L = _lib.load()
+    ones = np.ones(k, np.uint8)
+    h = ctypes.c_void_p()
+    assert L.ecw_matrix_codec_create(ones.ctypes.data_as(_lib._u8p), k, 1, 0, ctypes.byref(h)) == 0
+    try:
+        for n, ln in enumerate([1, 100, 4096, 5000, 3 * 1024 + 7, 65536]):
+            d = [orc.fill(ln, 300 + n, 0, j) for j in range(k)]
+            p = np.full(ln, 0x77, np.uint8)
+            dp = (ctypes.c_void_p * k)(*[x.ctypes.data for x in d])
+            pp = (ctypes.c_void_p * 1)(p.ctypes.data)
+            assert L.ecw_encode(h, dp, pp, ln) == 0
+            assert np.array_equal(p, orc.xor_blocks(d)), (k, ln)
+    finally:
+        L.ecw_codec_destroy(h)
