@@ -497,18 +497,83 @@ def small_calls(args):
         L.orc_encode_data_avx2(ln, k, m, tp, b[2], b[3])
 
     cpu = run_threads(1, max(args.small_calls_n, 20000), cpu_call)
+    seq = ecwide_h_sequence(args, shim, orc, ln)
     line = {
         "metric": "synchronous small encode calls GB/s (ECWide-H g_encode: ec_encode_data one 4 KiB chunk per call)",
         "value": gpu[0]["GBps"], "unit": "GB/s", "n_gpus": 1, "higher_is_better": True,
         "config": {"workload": f"RS-Cauchy k={k}, m={m}, {ln} B blocks, one stripe per synchronous call from each "
                                f"thread, through libecw_isal.so (ISA-L signatures) to the resident request service",
                    "bytes_per_call": (k + m) * ln},
-        "threads": gpu, "verified": bool(verified),
+        "threads": gpu, "verified": bool(verified), "ecwide_h_sequence": seq,
         "cpu_baseline": dict(cpu, value=cpu["GBps"], unit="GB/s", cores=1, kind="port",
                              sample="the same calls on the oracle's AVX2 port of ISA-L gf_3vect_dot_prod_avx2, "
                                     "1 thread", host_cpu=host_cpu_model()),
     }
     print(json.dumps(line), flush=True)
+
+
+def ecwide_h_sequence(args, shim, orc, ln: int) -> dict:
+    """ECWide-H's whole per-chunk call mix (ECWide-H/proxy/encode.cpp:113-238,
+    geometry common.hpp:21-32): l_encode (XOR of LK=11 through the all-ones
+    row of gf_gen_rs_matrix), g_encode (Cauchy GK=11 -> 3), l_middle (XOR of
+    NODE=4), l_decode (XOR of 5), each rebuilding its matrix and tables per
+    call as the reference does. GPU: the shim (the XOR calls take the
+    service's plain-XOR path); CPU: the same calls on the oracle's port."""
+    import ctypes
+    import threading
+
+    import numpy as np
+
+    u8p = ctypes.POINTER(ctypes.c_uint8)
+    # (sources, outputs, matrix generator rows, cauchy?)
+    calls = [(11, 1, False), (11, 3, True), (4, 1, False), (5, 1, False)]
+    nbytes = sum(k + m for k, m, _ in calls) * ln
+
+    def bufs():
+        rng = np.random.default_rng(args.seed + 1)
+        d = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(11)]
+        outs = [[np.zeros(ln, np.uint8) for _ in range(m)] for _, m, _ in calls]
+        dp = [(u8p * k)(*[x.ctypes.data_as(u8p) for x in d[:k]]) for k, _, _ in calls]
+        op = [(u8p * m)(*[x.ctypes.data_as(u8p) for x in o]) for (_, m, _), o in zip(calls, outs)]
+        mats = [np.zeros((k + m) * k, np.uint8) for k, m, _ in calls]
+        tbls = [np.zeros(32 * k * m, np.uint8) for k, m, _ in calls]
+        return d, outs, dp, op, mats, tbls
+
+    def run(gen_rs, gen_cauchy, init, encode, b):
+        _, _, dp, op, mats, tbls = b
+        for i, (k, m, cauchy) in enumerate(calls):
+            mp, tp = mats[i].ctypes.data_as(u8p), tbls[i].ctypes.data_as(u8p)
+            (gen_cauchy if cauchy else gen_rs)(mp, k + m, k)
+            init(k, m, mats[i][k * k:].ctypes.data_as(u8p), tp)
+            encode(ln, k, m, tp, dp[i], op[i])
+
+    L = orc.L
+    gpu_run = lambda b: run(shim.gf_gen_rs_matrix, shim.gf_gen_cauchy1_matrix, shim.ec_init_tables,
+                            shim.ec_encode_data, b)
+    cpu_run = lambda b: run(L.orc_gen_rs_matrix, L.orc_gen_cauchy1_matrix, L.orc_init_tables,
+                            L.orc_encode_data_avx2, b)
+    # parity of one sequence: GPU outputs == CPU outputs on the same inputs
+    bg, bc = bufs(), bufs()
+    gpu_run(bg)
+    cpu_run(bc)
+    verified = all(np.array_equal(x, y) for og, oc in zip(bg[1], bc[1]) for x, y in zip(og, oc))
+    n = max(1000, args.small_calls_n // 2)
+
+    def timed(fn, nt):
+        bs = [bufs() for _ in range(nt)]
+        th = [threading.Thread(target=lambda b=b: [fn(b) for _ in range(n)]) for b in bs]
+        t0 = time.perf_counter()
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
+        el = time.perf_counter() - t0
+        return {"threads": nt, "sequences": n * nt, "us_per_sequence_per_thread": round(el / n * 1e6, 2),
+                "GBps": round(n * nt * nbytes / el / 1e9, 3)}
+
+    return {"calls": "l_encode 11->1 XOR, g_encode 11->3 Cauchy, l_middle 4->1 XOR, l_decode 5->1 XOR, "
+                     "tables rebuilt per call", "bytes_per_sequence": nbytes, "verified": bool(verified),
+            "gpu": [timed(gpu_run, nt) for nt in (1, 4)], "cpu_port": timed(cpu_run, 1)}
 
 
 # ---- the bench ------------------------------------------------------------------

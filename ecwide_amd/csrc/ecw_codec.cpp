@@ -1044,21 +1044,26 @@ struct Service {
     return ECW_OK;
   }
 
+  // A slot's staging only grows (at least 1 MiB, doubling), and a replaced
+  // one is retired, not freed: freeing pinned memory can wait for the device
+  // to go idle, which the resident kernel does not while other callers keep
+  // it busy.
+  std::vector<void*> retired;
+
   int ensure_stage(int slot, size_t bytes) {
     if (stage_bytes[slot] >= bytes) return ECW_OK;
-    if (stage[slot]) (void)hipHostFree(stage[slot]);
-    stage[slot] = d_stage[slot] = nullptr;
-    stage_bytes[slot] = 0;
+    const size_t want = std::max({bytes, 2 * stage_bytes[slot], size_t(1) << 20});
     void* h = nullptr;
     void* dv = nullptr;
-    if (hipHostMalloc(&h, bytes, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return ECW_ENOMEM;
+    if (hipHostMalloc(&h, want, hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess) return ECW_ENOMEM;
     if (hipHostGetDevicePointer(&dv, h, 0) != hipSuccess) {
-      (void)hipHostFree(h);
+      retired.push_back(h);
       return ECW_EDEVICE;
     }
+    if (stage[slot]) retired.push_back(stage[slot]);
     stage[slot] = static_cast<uint8_t*>(h);
     d_stage[slot] = static_cast<uint8_t*>(dv);
-    stage_bytes[slot] = bytes;
+    stage_bytes[slot] = want;
     return ECW_OK;
   }
 
@@ -1136,8 +1141,15 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     }
     sv->cv.wait(lk, [&] { return !sv->free_slots.empty() || sv->broken; });
     if (sv->broken) return kNotServed;
-    slot = sv->free_slots.back();
-    sv->free_slots.pop_back();
+    // a thread keeps the slot it had last time when it is free: its parts
+    // poll at full speed (a slot idle for 1 ms polls slowly) and may still
+    // hold the thread's request words and tables
+    thread_local int t_slot = -1;
+    auto it = std::find(sv->free_slots.begin(), sv->free_slots.end(), t_slot);
+    if (it == sv->free_slots.end()) it = sv->free_slots.end() - 1;
+    slot = *it;
+    sv->free_slots.erase(it);
+    t_slot = slot;
     if (sv->ensure_stage(slot, cs * (k + np)) != ECW_OK) {
       sv->free_slots.push_back(slot);
       sv->cv.notify_one();

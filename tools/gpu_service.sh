@@ -7,6 +7,7 @@ tail -3 gpurun_out/pytest_service_$T.log
 cd tools/csrc && gcc -O2 -o /tmp/shim_bench shim_bench.c -L../../ecwide_amd -lecw_isal -lpthread -Wl,-rpath,$GRAFT_REPO_ROOT/ecwide_amd || exit 1
 cd $GRAFT_REPO_ROOT
 for t in 1 4 16; do timeout -k 10 120 /tmp/shim_bench $t 2000 >> gpurun_out/shim_bench_$T.log 2>&1 || exit $?; done
+for t in 1 4; do timeout -k 10 120 /tmp/shim_bench $t 1000 seq >> gpurun_out/shim_bench_$T.log 2>&1 || exit $?; done
 ECW_ISAL_BATCH=1 timeout -k 10 120 /tmp/shim_bench 4 2000 >> gpurun_out/shim_bench_$T.log 2>&1 || exit $?
 ECW_SERVICE=0 timeout -k 10 120 /tmp/shim_bench 1 2000 >> gpurun_out/shim_bench_$T.log 2>&1 || exit $?
 ECW_SERVICE=0 timeout -k 10 120 /tmp/shim_bench 4 2000 >> gpurun_out/shim_bench_$T.log 2>&1 || exit $?
