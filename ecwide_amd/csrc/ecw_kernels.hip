@@ -973,10 +973,10 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
       for (int spin = 1;; ++spin) {
         seq = sys_load_relaxed(&slot->seq);
         if (seq != last) break;
-        // a slot without a request for 1/20 of the idle exit polls less often:
+        // a part without work for 1/20 of the idle exit polls less often:
         // every poll is a PCIe read, and the reads of 128 busy pollers slow
-        // the hot slots' own polls and block reads (callers reuse the slot
-        // they released last, so one busy caller keeps one slot hot)
+        // the hot slots' own polls and block reads (a caller gets its slot
+        // back, so one busy caller keeps the parts of one slot hot)
         if (cold)
           for (int z = 0; z < ECW_SVC_COLD_SLEEPS; ++z) __builtin_amdgcn_s_sleep(127);
         if ((spin & 63) == 0) {
@@ -1002,7 +1002,6 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
     }
     __syncthreads();
     const unsigned long long seq = bcast[0];
-    served = static_cast<unsigned long long>(wall_clock64());
     if (bcast[1]) {
       if (part == 0 && threadIdx.x == 0) __hip_atomic_store(&ds->seq, kSvcLeave, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
       break;
@@ -1012,6 +1011,9 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
       __syncthreads();  // bcast is rewritten next round
       continue;
     }
+    // polling speed follows the requests this part had work in: with 4 KiB
+    // calls only parts 0-3 stay hot
+    served = static_cast<unsigned long long>(wall_clock64());
 #if ECW_SVC_TRACE
     trace[0] = static_cast<unsigned long long>(wall_clock64());
 #endif
