@@ -220,6 +220,27 @@
 #define ECW_LRESET_0
 #define ECW_LRESET_1 "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t"
 
+// Write window (EncodeGeom::wwidth > 0). A tile's parity stores wait until
+// the chip-wide 100 MHz constant clock (s_memrealtime: the same counter on
+// every CU) is in the first `wwidth` ticks of every `wmask + 1`. HBM pays for
+// each switch between reading and writing far more than for the written bytes
+// (1 output row per 128 read rows costs +9 % time); gathering every
+// workgroup's stores into the same short windows gives the memory long read
+// runs and short write bursts. A wave waits on its own (no workgroup barrier),
+// at most wmask + 1 ticks. Which layouts use it: launch_encode (ecw_kernels.hip).
+#define ECW_WRITE_WINDOW                                                     \
+  "s_cmp_eq_u32 %[ww], 0\n\t"                                               \
+  "s_cbranch_scc1 35f\n\t"                                                  \
+  "34:\n\t"                                                                 \
+  "s_memrealtime s[48:49]\n\t"                                              \
+  "s_waitcnt lgkmcnt(0)\n\t"                                                \
+  "s_and_b32 s48, s48, %[wmask]\n\t"                                        \
+  "s_cmp_lt_u32 s48, %[ww]\n\t"                                             \
+  "s_cbranch_scc1 35f\n\t"                                                  \
+  "s_sleep 2\n\t"                                                           \
+  "s_branch 34b\n\t"                                                        \
+  "35:\n\t"
+
 #ifndef ECW_ASM_DIAG_NOSTORE
 #define ECW_ASM_GSTORE(V, S) "global_store_dwordx4 v40, " V ", " S ECW_ASM_STMOD "\n\t"
 #else
@@ -297,6 +318,7 @@
   "s_waitcnt vmcnt(0)\n\t"                                                  \
   ECW_ROW_B(XL) BND                                                         \
   "13:\n\t"                                                                 \
+  ECW_WRITE_WINDOW                                                          \
   END                                                                       \
   /* global rows: byte l of the packed accumulators -> output row l */      \
   ECW_GPTR_INIT_##MODE                                                      \
@@ -335,7 +357,7 @@
 #define ECW_TILE_OPERANDS                                                          \
   : : [row0] "s"(row0), [lrow0] "s"(lrow0), [grow0] "s"(grow0), [bslo] "s"(bslo), \
     [bshi] "s"(bshi), [pbslo] "s"(pbslo), [pbshi] "s"(pbshi), [k] "s"(k), [r] "s"(r),  \
-    [nrows] "s"(nrows), [lds] "s"(lds),                                            \
+    [nrows] "s"(nrows), [lds] "s"(lds), [wmask] "s"(wmask), [ww] "s"(ww),          \
     [col] "v"(col)                                                                 \
   : "v4", "v5", "v6", "v7", "v8", "v9", "v10", "v11", "v12", "v13", "v14", "v15", "v16", "v17", "v18",  \
     "v19", "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27", "v28", "v29", "v30", "v31", "v32",  \
@@ -518,6 +540,7 @@
   "s_waitcnt vmcnt(0)\n\t"                                                  \
   ECW2_ROW_B(XL) BND                                                        \
   "13:\n\t"                                                                 \
+  ECW_WRITE_WINDOW                                                          \
   END                                                                       \
   /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \
   ECW_GPTR_INIT_##MODE                                                      \
@@ -597,7 +620,7 @@ namespace {
 template <int LOCAL, bool PARK, bool TAB, int NW = 1>
 __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
                                                 uint64_t pbstride, int k, int r, int nrows, uint32_t lds,
-                                                uint32_t col) {
+                                                uint32_t col, uint32_t wmask, uint32_t ww) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
   const uint32_t pbslo = static_cast<uint32_t>(pbstride), pbshi = static_cast<uint32_t>(pbstride >> 32);
   if constexpr (NW == 2) {

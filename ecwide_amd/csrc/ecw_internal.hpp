@@ -64,6 +64,7 @@ struct EncodeGeom {
   uint64_t tile_end;     //   (tile = stripe * tiles + column tile)
   unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter
   uint64_t ticket_base;        //   whose value at this launch's start is ticket_base
+  uint32_t wmask, wwidth;      // write window (asm tile): store when (clock & wmask) < wwidth; 0 = off
 };
 
 // Device counter of ticket-ordered encode launches, one per (codec, stream).

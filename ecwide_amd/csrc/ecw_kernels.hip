@@ -24,6 +24,9 @@
 // No MFMA: the work is byte-wise GF(2^8), not a dense FP contraction.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
 #include <type_traits>
 
 #include "ecw_internal.hpp"
@@ -402,6 +405,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
+  const uint32_t wmask = __builtin_amdgcn_readfirstlane(g.wmask), ww = __builtin_amdgcn_readfirstlane(g.wwidth);
   // the ticket slot sits after the tables: a static __shared__ variable would
   // shift the table records off the 64*NW alignment the LDS addressing relies on
   unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
@@ -416,7 +420,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
         const uint8_t* pb = uniform_ptr(rows.pbase + static_cast<uint64_t>(cur.s) * rows.psstride);
         encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * pbs),
                                                 const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * pbs), bs,
-                                                pbs, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+                                                pbs, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col, wmask, ww);
       } else if constexpr (std::is_same<Rows, PtrTabRows>::value) {
         // this stripe's rows of the device pointer tables, read with s_load
         const uint64_t s = static_cast<uint64_t>(cur.s);
@@ -424,7 +428,8 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
         const uint8_t* dt = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.dst + s * rows.np));
         encode_tile_asm<LOCAL, PARK, true, NW>(st, const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.m) * sizeof(void*)),
                                            const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.row0) * sizeof(void*)),
-                                           0, 0, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+                                           0, 0, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col,
+                                           wmask, ww);
       } else {
         const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
             reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
@@ -432,7 +437,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
         encode_tile_asm<LOCAL, PARK, true, NW>(ka + offsetof(PtrRows, src),
                                            const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
                                            const_cast<uint8_t*>(dtab), 0, 0, k, r, nrows,
-                                           __builtin_amdgcn_readfirstlane(lds_base), cur.col);
+                                           __builtin_amdgcn_readfirstlane(lds_base), cur.col, wmask, ww);
       }
     } else {
       uint4 ring[kPrefetchEncAsmTail];
@@ -665,6 +670,44 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 #define ECW_TICKET_MIN_TILES (4ull * 256 * ECW_GRID_PER_CU)
 #endif
 
+// Write window of the asm tile (ECW_WRITE_WINDOW in ecw_encode_asm.hpp): every
+// tile's parity stores wait for the first 64 of every 2048 ticks (0.64 us of
+// 20.5 us) of the 100 MHz constant clock. It pays for whole-block layouts,
+// where a column tile's parity stores go to m + g rows a block apart: encode
+// +4..7 % on the block slab (5678 -> 5910, 5538 -> 5948 GB/s), +5 % whole-block
+// split slab, +5.6 % pointer mode (profiles/r02_encode_write_window*.log;
+// 2^10..2^12-tick periods within 1 %, 2^13 and longer lock the workgroups into
+// generations that wait for the window: -6 %). The tiled slab (8 KiB column
+// pieces, a unit's parities one contiguous run) already writes in short
+// bursts: -1 % / +1.6 % on two boxes, so pieces under 64 KiB stay without it,
+// and so do launches under 8192 tiles (a window adds up to 20 us of latency).
+// ECW_WRITE_WINDOW = auto (default) | off | on | "LOG2P,W" overrides the choice
+// (tuning; read per launch).
+template <class Rows>
+inline bool window_auto(const Rows&, const EncodeGeom& g) {
+  return g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
+}
+
+template <class Rows>
+void set_write_window(const Rows& rows, EncodeGeom& g) {
+  uint32_t log2p = 11, w = 64;
+  bool on = window_auto(rows, g);
+  if (const char* e = std::getenv("ECW_WRITE_WINDOW")) {
+    unsigned a = 0, b = 0;
+    if (!std::strcmp(e, "off") || !std::strcmp(e, "0")) {
+      on = false;
+    } else if (!std::strcmp(e, "on")) {
+      on = true;
+    } else if (std::sscanf(e, "%u,%u", &a, &b) == 2 && a >= 4 && a <= 24 && b > 0) {
+      on = true;
+      log2p = a;
+      w = b;
+    }
+  }
+  g.wmask = (1u << log2p) - 1;
+  g.wwidth = on ? w : 0;
+}
+
 template <class Rows>
 hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s, TicketCounter* tc) {
   const uint64_t total = static_cast<uint64_t>(g0.stripes) * g0.tiles;
@@ -672,12 +715,14 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
   if (g0.nrows < 1 || g0.nrows > kMaxPassRows || g0.k < 1 || g0.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
   (void)hipGetLastError();  // report this call's launch errors, not an earlier one
   const uint4* tbl = static_cast<const uint4*>(d_tbl);
+  EncodeGeom gw = g0;
+  set_write_window(rows, gw);
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
                        : ECW_COHORT_TILES == 0 ? 256ull * ECW_GRID_PER_CU
                                                : total;
   if (tc && tc->ptr && encode_uses_ticket(total, g0.k)) {
     // one ticket-ordered launch; the caller holds the counter for this stream
-    EncodeGeom g = g0;
+    EncodeGeom g = gw;
     g.tile_begin = 0;
     g.tile_end = total;
     g.ticket = tc->ptr;
@@ -689,7 +734,7 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
     return e;
   }
   for (uint64_t t0 = 0; t0 < total; t0 += win) {
-    EncodeGeom g = g0;
+    EncodeGeom g = gw;
     g.ticket = nullptr;
     g.tile_begin = t0;
     g.tile_end = t0 + win < total ? t0 + win : total;

@@ -286,6 +286,55 @@ def test_ticket_launch_matches_windows(E, torch, orc, k, m, r, B, S, layout, loc
             assert torch.equal(p[-W:], first[n][i]), ("second encode", s, i)
 
 
+@pytest.mark.parametrize("k,m,r,local,layout", [
+    (32, 3, 11, "xor", "blocks"),     # parked locals (the bench shape's tile)
+    (32, 6, 8, "xor", "blocks"),      # 5-8 rows: the u64-entry (NW=2) tile
+    (24, 2, 3, "xor", "split"),       # 8 groups: mid-tile local stores
+    (16, 3, 4, "literal", "blocks"),  # zero L blocks
+    (32, 3, 11, "xor", "ptr"),        # device pointer tables
+])
+def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, layout):
+    """The write window (ecw_kernels.hip set_write_window) only delays the
+    parity stores: encodes with it forced off, on, and at another period give
+    identical parities, equal to the oracle on a column window, and the default
+    choice ('auto': on for whole blocks >= 64 KiB and >= 8192 tiles) is one of them."""
+    B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles: auto turns it on
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
+    np_ = c.parityNum
+    if layout == "ptr":  # data blocks of a filled slab, parities separate allocations
+        src = E.StripeSlab(c, stripes=S, block_bytes=B)
+        src.fill_random(seed=77)
+        data = [[src.block(s, j) for j in range(k)] for s in range(S)]
+    outs = {}
+    for env in ("off", "on", "10,32", None):
+        if env is None:
+            monkeypatch.delenv("ECW_WRITE_WINDOW", raising=False)
+        else:
+            monkeypatch.setenv("ECW_WRITE_WINDOW", env)
+        if layout == "ptr":
+            par = [[torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(np_)] for _ in range(S)]
+            E.BlockBatch(c, data, par).encode()
+            torch.cuda.synchronize()
+            outs[env] = [par[0], par[S - 1]]
+        else:
+            slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout=layout)
+            slab.fill_random(seed=77)
+            slab.encode()
+            torch.cuda.synchronize()
+            outs[env] = [[p.clone() for p in slab.parity(s)] for s in (0, S - 1)]
+            del slab
+    for env in ("on", "10,32", None):
+        for n in range(2):
+            for i in range(np_):
+                assert torch.equal(outs[env][n][i], outs["off"][n][i]), (env, n, i)
+    W = 8192
+    oc = orc.codec("C", k, m, r, W)
+    for n, s in enumerate((0, S - 1)):
+        want = oc.encode([orc.fill(W, 77, s, j, B - W) for j in range(k)], literal=local == "literal")
+        for i, w in enumerate(want):
+            assert np.array_equal(outs["on"][n][i][B - W:].cpu().numpy(), w), (s, i)
+
+
 def test_full_size_tiled_bench_path(E, torch, manifest):
     """The bench's timed bytes at the bench's size: tiled slab, CL(128, 27, 3),
     64 MiB blocks, 8 stripes, seed 103. Stripe 0 is the stripe of manifest

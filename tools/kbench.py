@@ -3,6 +3,10 @@
 same data, rounds interleaved: cdna_hip_programming.md §5.4 rule 24).
 
   python tools/kbench.py [--k 128 --m 3 --r 27 --mib 64 --stripes 4 --rounds 5] build/variants/*.so
+
+A lib given as PATH@VALUE runs with ECW_WRITE_WINDOW=VALUE set around its calls
+(the encode's write-window choice is read per launch), so one build can be
+A/B-ed against itself: ecwide_amd/libecwide.so@off ecwide_amd/libecwide.so@on.
 """
 import argparse
 import ctypes
@@ -57,13 +61,17 @@ def main():
     out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
     stream = c_void_p(torch.cuda.current_stream().cuda_stream)
     libs = []
-    for path in a.libs:
+    envs = {}
+    for spec in a.libs:
+        path, _, env = spec.partition("@")
         L = _lib.load(path, strict=False)
         sch = _lib.ecw_scheme()
         assert L.ecw_scheme_init(byref(sch), a.code.encode(), k, m, r, B) == 0
         h = c_void_p()
         assert L.ecw_codec_create(byref(sch), 1, 0, 1 if a.literal else 0, 0, byref(h)) == 0
-        libs.append((os.path.basename(path), L, h))
+        name = os.path.basename(path) + (f"@{env}" if env else "")
+        envs[name] = env
+        libs.append((name, L, h))
     L0 = libs[0][1]
     if a.split:
         assert a.chunk and a.pad == 0, "--split needs --chunk and --pad 0"
@@ -87,6 +95,10 @@ def main():
     res = {n: ([], []) for n, _, _ in libs}
     for rd in range(a.rounds):
         for name, L, h in libs:
+            if envs[name]:
+                os.environ["ECW_WRITE_WINDOW"] = envs[name]
+            else:
+                os.environ.pop("ECW_WRITE_WINDOW", None)
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             for it in range(a.iters + 1):
                 if it == 1:
