@@ -399,8 +399,12 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
     const Rows rows, const EncodeGeom g, const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int n16 = g.k * 8 * NW;
+#ifndef ECW_DIAG_NOSTAGE  // diagnostic builds only: time the encode without staging its tables
   for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
   __syncthreads();
+#else
+  (void)n16;
+#endif
   const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);

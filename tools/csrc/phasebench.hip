@@ -94,11 +94,34 @@ __device__ __forceinline__ void write_tile(const Geo& g, uint64_t t, const u32x4
   for (int i = 0; i < NOUT; ++i) stnt(p + (uint64_t)i * g.bstride, acc[i]);
 }
 
-// one tile per workgroup, stores right after the reads (the encode's pattern)
-template <bool ST>
+// read ring of depth D (loads in flight per lane)
+template <int D>
+__device__ __forceinline__ void read_tile_d(const Geo& g, uint64_t t, u32x4* acc) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = u32x4{0, 0, 0, 0};
+  const uint8_t* p = rowp(g, t, 0);
+  u32x4 v[D];
+#pragma unroll
+  for (int d = 0; d < D; ++d) v[d] = ldnt(p + (uint64_t)d * g.bstride);
+  for (int j = 0; j < g.k - D; j += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      acc[(j + d) & 7] ^= v[d];
+      v[d] = ldnt(p + (uint64_t)(j + D + d) * g.bstride);
+    }
+  }
+#pragma unroll
+  for (int d = 0; d < D; ++d) acc[d & 7] ^= v[d];
+}
+
+// one tile per workgroup, stores right after the reads (the encode's pattern);
+// dynamic LDS (unused) sets the occupancy; D = read ring depth
+template <bool ST, int D = 2>
 __global__ __launch_bounds__(256) void inter_kernel(Geo g, uint32_t* sink) {
+  extern __shared__ u32x4 lds_occ[];
   u32x4 acc[8];
-  read_tile(g, blockIdx.x, acc);
+  if (D == 2) read_tile(g, blockIdx.x, acc); else read_tile_d<D>(g, blockIdx.x, acc);
+  if (g.k < 0) lds_occ[threadIdx.x] = acc[0];
   if (ST) {
     write_tile(g, blockIdx.x, acc);
   } else {
@@ -307,29 +330,17 @@ int main(int argc, char** argv) {
       run_phased<0, 1>(g, ctr, fail, 2, iters, sbytes);
       run_phased<0, 1>(g, ctr, fail, 4, iters, sbytes);
     }
-    // write windows, per-wave polling, power-of-two periods
-    for (unsigned P : {2048u, 4096u, 8192u})
-      for (unsigned W : {P / 32}) {
-        double wms = time_ms([&] { window_kernel<true><<<(unsigned)g.ntiles, 256>>>(g, P, W); }, iters);
-        std::printf("wave window %4u of %5u ticks   %8.1f GB/s (136 rows counted)\n", W, P, sbytes / wms / 1e6);
-      }
-    // pipelined: persistent grid, pending outputs stored in the next window
-    for (int div : {1, 2}) {
-      int dev = 0, ncu = 0, per_cu = 0;
-      CHECK(hipGetDevice(&dev));
-      CHECK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-      CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, pipelined_kernel<8>, 256, 0));
-      const unsigned grid = ncu * (per_cu / div);
-      for (unsigned P : {1024u, 2048u, 4096u, 8192u, 16384u})
-        for (unsigned W : {P / 32, P / 16, P}) {
-          if (W == P && P != 1024u) continue;
-          double wms = time_ms([&] { pipelined_kernel<8><<<grid, 256>>>(g, P, W); }, iters);
-          std::printf("pipelined grid %u (%d/CU) window %5u of %5u   %8.1f GB/s (136 rows counted)\n", grid,
-                      per_cu / div, W, P, sbytes / wms / 1e6);
-        }
+    // read-only and interleaved rates against occupancy (dynamic LDS) and ring depth
+    for (int lds : {0, 24576, 36864}) {
+      double r2 = time_ms([&] { inter_kernel<false, 2><<<(unsigned)g.ntiles, 256, lds>>>(g, sink); }, iters);
+      double r4 = time_ms([&] { inter_kernel<false, 4><<<(unsigned)g.ntiles, 256, lds>>>(g, sink); }, iters);
+      double s2 = time_ms([&] { inter_kernel<true, 2><<<(unsigned)g.ntiles, 256, lds>>>(g, sink); }, iters);
+      double s4 = time_ms([&] { inter_kernel<true, 4><<<(unsigned)g.ntiles, 256, lds>>>(g, sink); }, iters);
+      std::printf("lds %5d: read-only ring2 %7.1f ring4 %7.1f | with stores ring2 %7.1f ring4 %7.1f (136 rows counted)\n",
+                  lds, sbytes / r2 / 1e6, sbytes / r4 / 1e6, sbytes / s2 / 1e6, sbytes / s4 / 1e6);
     }
     // the repair's mix: 27 rows -> 1 row
-    {
+    if (argc > 4) {
       Geo r = g;
       r.k = 27;  // same geometry (rows 0..27 of each unit: inside it in both layouts)
       const double rbytes = (double)S * 28 * B;
