@@ -685,11 +685,17 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 // pieces, a unit's parities one contiguous run) already writes in short
 // bursts: -1 % / +1.6 % on two boxes, so pieces under 64 KiB stay without it,
 // and so do launches under 8192 tiles (a window adds up to 20 us of latency).
+// Narrow stripes lose: the window re-synchronises the resident workgroups into
+// generations whose time is rounded up to whole periods, which costs more
+// than it saves when a tile's reads take only a few periods (block slab k=32
+// -4 %, pointer mode k=32 -8 %, k=8 -47 %; k=64 +5.5 %, k=96 +4.2 %, k=200 +7 %,
+// RS(128, 3) +3.1 %; profiles/r02_encode_write_window_k*.log), so only k >= 64
+// uses it, and not the 5-8-row tile (4 waves per SIMD: -1.2 %).
 // ECW_WRITE_WINDOW = auto (default) | off | on | "LOG2P,W" overrides the choice
 // (tuning; read per launch).
 template <class Rows>
 inline bool window_auto(const Rows&, const EncodeGeom& g) {
-  return g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
+  return g.k >= 64 && g.nrows <= 4 && g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
 }
 
 template <class Rows>

@@ -287,7 +287,7 @@ def test_ticket_launch_matches_windows(E, torch, orc, k, m, r, B, S, layout, loc
 
 
 @pytest.mark.parametrize("k,m,r,local,layout", [
-    (32, 3, 11, "xor", "blocks"),     # parked locals (the bench shape's tile)
+    (128, 3, 27, "xor", "blocks"),    # parked locals (the bench shape's tile); auto = on
     (32, 6, 8, "xor", "blocks"),      # 5-8 rows: the u64-entry (NW=2) tile
     (24, 2, 3, "xor", "split"),       # 8 groups: mid-tile local stores
     (16, 3, 4, "literal", "blocks"),  # zero L blocks
@@ -297,8 +297,8 @@ def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, lay
     """The write window (ecw_kernels.hip set_write_window) only delays the
     parity stores: encodes with it forced off, on, and at another period give
     identical parities, equal to the oracle on a column window, and the default
-    choice ('auto': on for whole blocks >= 64 KiB and >= 8192 tiles) is one of them."""
-    B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles: auto turns it on
+    choice ('auto': on for k >= 64 and <= 4 global rows, whole blocks >= 64 KiB and >= 8192 tiles) is one of them."""
+    B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
     np_ = c.parityNum
     if layout == "ptr":  # data blocks of a filled slab, parities separate allocations
