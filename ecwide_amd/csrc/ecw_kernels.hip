@@ -678,13 +678,14 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 // tile's parity stores wait for the first 64 of every 2048 ticks (0.64 us of
 // 20.5 us) of the 100 MHz constant clock. It pays for whole-block layouts,
 // where a column tile's parity stores go to m + g rows a block apart: encode
-// +4..7 % on the block slab (5678 -> 5910, 5538 -> 5948 GB/s), +5 % whole-block
-// split slab, +5.6 % pointer mode (profiles/r02_encode_write_window*.log;
-// 2^10..2^12-tick periods within 1 %, 2^13 and longer lock the workgroups into
-// generations that wait for the window: -6 %). The tiled slab (8 KiB column
-// pieces, a unit's parities one contiguous run) already writes in short
-// bursts: -1 % / +1.6 % on two boxes, so pieces under 64 KiB stay without it,
-// and so do launches under 8192 tiles (a window adds up to 20 us of latency).
+// +4..7 % on the block slab (5678 -> 5910, 5538 -> 5948 GB/s), +5.6 % pointer
+// mode, +10 % pointer tables over separate allocations (5386 -> 5920)
+// (profiles/r02_encode_write_window*.log; 2^10..2^12-tick periods within 1 %,
+// 2^13 and longer lock the workgroups into generations that wait for the
+// window: -6 %). Layouts whose parities sit in a region of their own gain
+// nothing reliable: tiled slab -2.1 / +1.6 / -0.9 %, whole-block split slab +5 /
+// -2.4 % on different boxes, so slabs use it only with in-slab parities.
+// Launches under 8192 tiles go without (a window adds up to 20 us of latency).
 // Narrow stripes lose: the window re-synchronises the resident workgroups into
 // generations whose time is rounded up to whole periods, which costs more
 // than it saves when a tile's reads take only a few periods (block slab k=32
@@ -693,10 +694,16 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 // uses it, and not the 5-8-row tile (4 waves per SIMD: -1.2 %).
 // ECW_WRITE_WINDOW = auto (default) | off | on | "LOG2P,W" overrides the choice
 // (tuning; read per launch).
-template <class Rows>
-inline bool window_auto(const Rows&, const EncodeGeom& g) {
+inline bool window_shape(const EncodeGeom& g) {
   return g.k >= 64 && g.nrows <= 4 && g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
 }
+// slabs: only with the parity rows in the slab after each stripe's data rows
+inline bool window_auto(const SlabRows& r, const EncodeGeom& g) {
+  return window_shape(g) && r.pbstride == r.bstride && r.psstride == r.sstride &&
+         r.pbase == r.base + static_cast<uint64_t>(g.k) * r.bstride;
+}
+inline bool window_auto(const PtrRows&, const EncodeGeom& g) { return window_shape(g); }
+inline bool window_auto(const PtrTabRows&, const EncodeGeom& g) { return window_shape(g); }
 
 template <class Rows>
 void set_write_window(const Rows& rows, EncodeGeom& g) {

@@ -42,7 +42,11 @@ def main():
     ap.add_argument("--split", action="store_true",
                     help="with --chunk: data chunks in one region, parities in another "
                          "(ecw_encode_batch_split_dev; encode only)")
+    ap.add_argument("--tables", action="store_true",
+                    help="pointer tables over separately allocated blocks (ecw_encode_ptrs_dev, the "
+                         "bench's pointer leg; encode only)")
     a = ap.parse_args()
+    assert not (a.tables and (a.check or a.split or a.ptr or a.chunk)), "--tables runs alone"
     import torch
 
     from ecwide_amd import _lib
@@ -80,6 +84,16 @@ def main():
         pbuf = torch.empty(S * (m + g) * B, dtype=torch.uint8, device="cuda")
         bstride, sstride = B, k * B
     assert L0.ecw_fill_random_dev(0, c_void_p(buf.data_ptr()), bstride, sstride, S, k, B, 1, 0, 0, stream) == 0
+    if a.tables:
+        del buf
+        blocks = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(S * nblk)]
+        for t in blocks[:S * k]:
+            t.random_(0, 256)
+        dtab = torch.tensor([blocks[s_ * nblk + j].data_ptr() for s_ in range(S) for j in range(k)],
+                            dtype=torch.int64, device="cuda")
+        ptab = torch.tensor([blocks[s_ * nblk + k + i].data_ptr() for s_ in range(S) for i in range(m + g)],
+                            dtype=torch.int64, device="cuda")
+        buf = blocks[0]
     enc_bytes = S * nblk * B
     rep_bytes = S * (r + 1) * B
     ref = None
@@ -103,7 +117,10 @@ def main():
             for it in range(a.iters + 1):
                 if it == 1:
                     e[0].record()
-                if a.split:
+                if a.tables:
+                    st = L.ecw_encode_ptrs_dev(h, S, c_void_p(dtab.data_ptr()), c_void_p(ptab.data_ptr()), B, stream)
+                    assert st == 0, (name, st)
+                elif a.split:
                     st = L.ecw_encode_batch_split_dev(h, c_void_p(buf.data_ptr()), B, k * B,
                                                       c_void_p(pbuf.data_ptr()), B, (m + g) * B, S, B, stream)
                     assert st == 0, (name, st)
@@ -115,7 +132,7 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split else 0  # literal L: no repair
+            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split and not a.tables else 0  # literal L: no repair
             for it in range(rep_iters):
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
                                             c_void_p(out.data_ptr()), B, B, stream)
