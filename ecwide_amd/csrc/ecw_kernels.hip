@@ -77,8 +77,11 @@ typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
 template <bool TAIL, bool NT = false>
 __device__ __forceinline__ uint4 ld16(const uint8_t* row, uint32_t col, uint32_t len) {
   if (NT && (!TAIL || col + 16 <= len)) {
+    // global address space: a pointer loaded from a table would otherwise be
+    // generic and get flat loads (which also count against lgkmcnt)
     typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(row + col));
+    typedef const __attribute__((address_space(1))) u32x4 gu32x4;
+    const u32x4 v = __builtin_nontemporal_load((gu32x4*)(row + col));
     return make_uint4(v.x, v.y, v.z, v.w);
   }
 #if ECW_BUFLOAD
@@ -121,8 +124,9 @@ __device__ __forceinline__ void st16(uint8_t* row, uint32_t col, uint32_t len, u
   if (!TAIL || col + 16 <= len) {
     if (NT || ECW_NT_STORES) {
       typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+      typedef __attribute__((address_space(1))) u32x4 gu32x4;
       const u32x4 w = {v.x, v.y, v.z, v.w};
-      __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(row + col));
+      __builtin_nontemporal_store(w, (gu32x4*)(row + col));
     } else {
       *reinterpret_cast<uint4*>(row + col) = v;
     }
@@ -460,10 +464,30 @@ __device__ __forceinline__ const uint8_t* xsrc(const XorSplit& a, int s, int i) 
   if (i < a.ndata) return a.base + s * a.sstride + static_cast<uint64_t>(a.idx[i]) * a.bstride;
   return a.pbase + s * a.psstride + static_cast<uint64_t>(a.idx[i]) * a.pbstride;
 }
-__device__ __forceinline__ const uint8_t* xsrc(const XorTab& a, int s, int i) {
-  return a.src[static_cast<uint64_t>(s) * a.n + i];
+// Pointer tables are read through the constant address space at a uniform
+// address, so the block pointers come in with scalar loads (batched by the
+// compiler) instead of one vector load per lane and source, each of which the
+// source's data loads had to wait for.
+#ifndef ECW_XORTAB_SCALAR
+#define ECW_XORTAB_SCALAR 1
+#endif
+template <class T>
+__device__ __forceinline__ T* uniform_table_entry(T* const* table, uint64_t index) {
+#if ECW_XORTAB_SCALAR
+  const uint64_t a = reinterpret_cast<uint64_t>(table + index);
+  const uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a));
+  const uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(a >> 32));
+  const __attribute__((address_space(4))) uint64_t* c =
+      reinterpret_cast<const __attribute__((address_space(4))) uint64_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+  return reinterpret_cast<T*>(*c);
+#else
+  return table[index];
+#endif
 }
-__device__ __forceinline__ uint8_t* xdst(const XorTab& a, int s) { return a.dst[s]; }
+__device__ __forceinline__ const uint8_t* xsrc(const XorTab& a, int s, int i) {
+  return uniform_table_entry(a.src, static_cast<uint64_t>(s) * a.n + i);
+}
+__device__ __forceinline__ uint8_t* xdst(const XorTab& a, int s) { return uniform_table_entry(a.dst, static_cast<uint64_t>(s)); }
 __device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
 __device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }
 __device__ __forceinline__ uint8_t* xdst(const XorSplit& a, int s) { return a.out + s * a.ostride; }
@@ -519,11 +543,20 @@ __device__ __forceinline__ void xor_tile_fixed(const Args& a, const XorGeom& g, 
   constexpr int W = ECW_XOR_WINDOW > 0 && ECW_XOR_WINDOW < N ? ECW_XOR_WINDOW : N;
   uint4 v[N];
   uint4 acc = make_uint4(0, 0, 0, 0);
+  // pointer tables: every source pointer first (one batch of scalar loads)
+  const uint8_t* sp[std::is_same<Args, XorTab>::value ? N : 1];
+  if constexpr (std::is_same<Args, XorTab>::value) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) sp[i] = xsrc(a, s, i);
+  }
   // the scheduling barriers pin the issue order (the machine scheduler would
   // otherwise pull the first XORs up between the first loads: vmcnt(0) after two)
 #pragma unroll
   for (int i = 0; i < N; ++i) {
-    v[i] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, i), col, len);
+    if constexpr (std::is_same<Args, XorTab>::value)
+      v[i] = ld16<TAIL, ECW_XOR_NT>(sp[i], col, len);
+    else
+      v[i] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, i), col, len);
     __builtin_amdgcn_sched_barrier(0);
     if (i >= W - 1) {
       acc = xor4(acc, v[i - W + 1]);

@@ -94,8 +94,15 @@ def main():
         ptab = torch.tensor([blocks[s_ * nblk + k + i].data_ptr() for s_ in range(S) for i in range(m + g)],
                             dtype=torch.int64, device="cuda")
         buf = blocks[0]
+        idx = (ctypes.c_int * 256)()
+        nsrc = L0.ecw_repair_sources(libs[0][2], 0, idx, 256)
+        assert nsrc > 0
+        stab = torch.tensor([blocks[s_ * nblk + idx[i]].data_ptr() for s_ in range(S) for i in range(nsrc)],
+                            dtype=torch.int64, device="cuda")
+        outs = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(S)]
+        otab = torch.tensor([o.data_ptr() for o in outs], dtype=torch.int64, device="cuda")
     enc_bytes = S * nblk * B
-    rep_bytes = S * (r + 1) * B
+    rep_bytes = S * (r + 1) * B  # --tables: nsrc = r sources + 1 output as well
     ref = None
     if a.check:
         assert libs[0][1].ecw_encode_batch_dev(libs[0][2], c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream) == 0
@@ -132,8 +139,13 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split and not a.tables else 0  # literal L: no repair
+            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split else 0  # literal L: no repair
             for it in range(rep_iters):
+                if a.tables:
+                    st = L.ecw_xor_reduce_ptrs_dev(0, S, nsrc, c_void_p(stab.data_ptr()), c_void_p(otab.data_ptr()),
+                                                   B, stream)
+                    assert st == 0, (name, st)
+                    continue
                 st = L.ecw_repair_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, 0,
                                             c_void_p(out.data_ptr()), B, B, stream)
                 assert st == 0, (name, st)
