@@ -227,15 +227,20 @@
 // (1 output row per 128 read rows costs +9 % time); gathering every
 // workgroup's stores into the same short windows gives the memory long read
 // runs and short write bursts. A wave waits on its own (no workgroup barrier),
-// at most wmask + 1 ticks. Which layouts use it: launch_encode (ecw_kernels.hip).
+// at most wmask + 1 ticks (and at most 16384 polls, whatever the clock does).
+// Which layouts use it: launch_encode (ecw_kernels.hip).
 #define ECW_WRITE_WINDOW                                                     \
   "s_cmp_eq_u32 %[ww], 0\n\t"                                               \
   "s_cbranch_scc1 35f\n\t"                                                  \
+  "s_mov_b32 s47, 0\n\t"                                                    \
   "34:\n\t"                                                                 \
   "s_memrealtime s[48:49]\n\t"                                              \
   "s_waitcnt lgkmcnt(0)\n\t"                                                \
   "s_and_b32 s48, s48, %[wmask]\n\t"                                        \
   "s_cmp_lt_u32 s48, %[ww]\n\t"                                             \
+  "s_cbranch_scc1 35f\n\t"                                                  \
+  "s_add_u32 s47, s47, 1\n\t"                                               \
+  "s_cmp_gt_u32 s47, 0x4000\n\t"        /* bound: never wait unboundedly */ \
   "s_cbranch_scc1 35f\n\t"                                                  \
   "s_sleep 2\n\t"                                                           \
   "s_branch 34b\n\t"                                                        \
