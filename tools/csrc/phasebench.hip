@@ -65,6 +65,8 @@ struct Geo {
   uint8_t* base;
   uint64_t bstride, sstride, tps, ntiles;
   int k;
+  uint8_t* pbase = nullptr;  // non-null: output rows in a region of their own
+  uint64_t pbstride = 0, psstride = 0;
 };
 
 __device__ __forceinline__ uint8_t* rowp(const Geo& g, uint64_t t, int j) {
@@ -89,6 +91,13 @@ __device__ __forceinline__ void read_tile(const Geo& g, uint64_t t, u32x4* acc) 
 
 template <int NOUT = 8>
 __device__ __forceinline__ void write_tile(const Geo& g, uint64_t t, const u32x4* acc) {
+  if (g.pbase) {
+    const uint64_t su = t / g.tps, c = t % g.tps;
+    uint8_t* q = g.pbase + su * g.psstride + c * 4096 + threadIdx.x * 16;
+#pragma unroll
+    for (int i = 0; i < NOUT; ++i) stnt(q + (uint64_t)i * g.pbstride, acc[i]);
+    return;
+  }
   uint8_t* p = rowp(g, t, g.k);
 #pragma unroll
   for (int i = 0; i < NOUT; ++i) stnt(p + (uint64_t)i * g.bstride, acc[i]);
@@ -298,6 +307,18 @@ int main(int argc, char** argv) {
     g.ntiles = (uint64_t)S * (B / 4096);
     std::printf("geometry: tiled (rows 8 KiB apart)\n");
   }
+  if (argc > 3 && std::atoi(argv[3]) == 2) {
+    // the bench's tiled slab: (stripe, piece) units of k x 8 KiB data, their 8
+    // parity pieces one 64 KiB run in a region after all the data
+    g.bstride = 8192;
+    g.sstride = (uint64_t)k * 8192;
+    g.tps = 2;
+    g.ntiles = (uint64_t)S * (B / 4096);
+    g.pbase = buf + (uint64_t)S * k * B;
+    g.pbstride = 8192;
+    g.psstride = 8 * 8192;
+    std::printf("geometry: tiled, parities in their own region (the bench's slab)\n");
+  }
   const double sbytes = (double)S * (k + 8) * B;
   const bool sweep_barriers = argc > 2 && std::atoi(argv[2]) == 1;
   for (int rep = 0; rep < 2; ++rep) {
@@ -329,6 +350,13 @@ int main(int argc, char** argv) {
       run_phased<1, 1>(g, ctr, fail, 1, iters, sbytes);
       run_phased<0, 1>(g, ctr, fail, 2, iters, sbytes);
       run_phased<0, 1>(g, ctr, fail, 4, iters, sbytes);
+    }
+    for (unsigned P : {2048u, 4096u, 8192u}) {
+      const unsigned W = P / 32;
+      double wms = time_ms([&] { window_kernel<true><<<(unsigned)g.ntiles, 256>>>(g, P, W); }, iters);
+      double w6 = time_ms([&] { window_kernel<true><<<(unsigned)g.ntiles, 256, 24576>>>(g, P, W); }, iters);
+      std::printf("wave window %4u of %5u ticks   %8.1f GB/s, at 6 WG/CU %8.1f (136 rows counted)\n", W, P,
+                  sbytes / wms / 1e6, sbytes / w6 / 1e6);
     }
     // read-only and interleaved rates against occupancy (dynamic LDS) and ring depth
     for (int lds : {0, 24576, 36864}) {
