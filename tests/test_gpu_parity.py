@@ -479,16 +479,17 @@ def test_block_batch_encode_repair(E, torch, orc):
             assert torch.equal(out[s], want), (lost, s)
 
 
-def test_encode_ptrs_dev_ticket_and_errors(E, torch, orc):
+@pytest.mark.parametrize("k,m,r,B,S", [(4, 2, 2, 256 << 20, 4), (64, 2, 32, 64 << 20, 16)])
+def test_encode_ptrs_dev_ticket_and_errors(E, torch, orc, k, m, r, B, S):
     """>= 262,144 tiles through the pointer tables take the ticket-ordered
     launch (twice on one stream: the counter carries over); the result equals
-    the split slab's encode of the same bytes. Misaligned tables and m = 0
-    are refused."""
+    the split slab's encode of the same bytes. At k = 64 the pointer-table
+    launch also holds its stores for the write window (the split slab does
+    not), 68 GiB. Misaligned tables and m = 0 are refused."""
     from ctypes import c_void_p
 
     from ecwide_amd._lib import lib
 
-    k, m, r, B, S = 4, 2, 2, 256 << 20, 4
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
     slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout="split")
     slab.fill_random(seed=8)
@@ -501,6 +502,10 @@ def test_encode_ptrs_dev_ticket_and_errors(E, torch, orc):
     for s in range(S):
         for i, p in enumerate(slab.parity(s)):
             assert torch.equal(p, par[s][i]), (s, i)
+    if k != 4:
+        del slab, batch, par
+        torch.cuda.empty_cache()
+        return
     st = lib.ecw_encode_ptrs_dev(c._h, S, c_void_p(batch.dtab.data_ptr() + 4), c_void_p(batch.ptab.data_ptr()), B,
                                  c_void_p(torch.cuda.current_stream().cuda_stream))
     assert st == -4
