@@ -257,7 +257,10 @@
 #define ECW_ASM_LSTORE  // diagnostic builds only: time the encode without its local-parity stores
 #endif
 #ifndef ECW_ASM_STMOD
-#define ECW_ASM_STMOD " nt"  // parity stores: nontemporal (+3 % encode, measured)
+// parity stores: nontemporal (+3 % encode over plain stores, round 1) at system
+// scope (sc0 sc1: +0.4..0.7 % over nt alone on the tiled slab in three
+// processes, +0.5 % block slab; profiles/r02_encode_store_policy_ab.log)
+#define ECW_ASM_STMOD " nt sc0 sc1"
 #endif
 #ifndef ECW_ASM_LDMOD
 #define ECW_ASM_LDMOD " nt"  // ring loads: nontemporal, every byte is read once (+2 %, measured)
