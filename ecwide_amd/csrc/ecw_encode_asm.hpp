@@ -263,7 +263,9 @@
 #define ECW_ASM_STMOD " nt sc0 sc1"
 #endif
 #ifndef ECW_ASM_LDMOD
-#define ECW_ASM_LDMOD " nt"  // ring loads: nontemporal, every byte is read once (+2 %, measured)
+// ring loads: nontemporal, every byte is read once (+2 %, measured); nt sc1 /
+// nt sc0 sc1 the same, sc0 sc1 without nt -9 % (profiles/r02_encode_load_policy_ab.log)
+#define ECW_ASM_LDMOD " nt"
 #endif
 #define ECW_LOAD_A "global_load_dwordx4 v[4:7], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_LOAD_B "global_load_dwordx4 v[8:11], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
