@@ -8,13 +8,22 @@ Algorithmic bytes per stripe: encode (k+m+g)*B, repair (r+1)*B (inputs +
 outputs, ISA-L's perf_print convention). GB = 1e9.
 
 Workloads (BASELINE.json configs):
-  * N=1 default — configs[2] shape: CL(k=128, r=27, m=3), 64 MiB blocks,
-    8 stripes (the metric's k=128 / 64 MiB point); stripe 0 is the stripe the
-    committed full-size digests pin (seed 103, tests/golden/manifest.json).
-  * N>1 default — configs[4]: the configs[3] batch (256 stripes, block size
-    sized so the whole batch fills ONE GPU's HBM) split by stripe over the N
-    ranks, same B at every N ("scaling": "strong"). `--weak` gives every rank
-    the N=1 slab instead; `--hbm-fill` runs configs[3] at N=1.
+  * `value`, at every N — the metric's point, configs[2]'s shape: CL(k=128,
+    r=27, m=3), 64 MiB blocks, 8 stripes PER GPU ("scaling": "weak"), so
+    the N=1 line (= BENCH) and every N>1 line of the 1/2/4/8 curve measure
+    the same per-GPU workload; stripe 0 is the stripe the committed
+    full-size digests pin (seed 103, tests/golden/manifest.json).
+  * `configs4`, a second timed leg in the same line: the configs[3] batch
+    (256 stripes, block size sized so the whole batch fills ONE GPU's HBM,
+    the same B at every N) split by stripe over the N GPUs ("strong"; at
+    N=1 it is configs[3] itself).
+  * `other_layout` (N=1): the same workload in the reference's block
+    layouts (split slab, pointer tables over separately allocated blocks),
+    interleaved round by round with the tiled slab in one process.
+  * `host_resident` (rank 0): the PCIe-inclusive rate (pinned host blocks,
+    hipMemcpyAsync in and out) and the ChunkGenerator replay timed around
+    encodeChunks as ChunkGenerator.java:126-131 times it.
+  `--hbm-fill` makes configs[3] the main leg, `--strong` splits --stripes.
 
 Multi-GPU: `python bench.py --gpus N` starts N rank processes itself
 (torch.distributed.run in a child process, before any GPU call in this one)
@@ -49,9 +58,14 @@ def parse(argv=None):
                     help="slab layout in HBM (ecwide_amd/slab.py): tiled (default; each --chunk-kib column piece "
                          "of the k data blocks contiguous, parities apart), split (whole blocks, parity blocks in "
                          "a region of their own) or blocks (whole blocks, [D.., G.., L..] per stripe)")
-    ap.add_argument("--other-layout-steps", type=int, default=5,
-                    help="N=1: also time this many steps with whole blocks (split slab, pointer mode) and report "
-                         "them in the line (0 = off)")
+    ap.add_argument("--other-layout-steps", type=int, default=2,
+                    help="N=1: encode + repair steps per layout and round in the whole-block legs (split slab, "
+                         "pointer tables), interleaved with the tiled slab (0 = off)")
+    ap.add_argument("--other-layout-rounds", type=int, default=4, help="rounds of the interleaved layout legs")
+    ap.add_argument("--configs4-steps", type=int, default=5,
+                    help="timed steps of the configs[3]/[4] HBM-filling leg reported as `configs4` (0 = off)")
+    ap.add_argument("--host-iters", type=int, default=2,
+                    help="rank 0: encodes + repairs of the PCIe-inclusive host-resident leg (0 = off)")
     ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
     ap.add_argument("--unit-pad", type=int, default=0, help="tiled layout: padding after each piece run (bytes)")
     ap.add_argument("--steps", type=int, default=20)
@@ -60,7 +74,7 @@ def parse(argv=None):
     ap.add_argument("--m", type=int, default=3)
     ap.add_argument("--r", type=int, default=27)
     ap.add_argument("--block-mib", type=float, default=None, help="block size (default 64; --hbm-fill: from free HBM)")
-    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (weak) or in total (strong); default 8")
+    ap.add_argument("--stripes", type=int, default=None, help="stripes per GPU (weak) or in total (--strong); default 8")
     ap.add_argument("--seed", type=int, default=DEFAULT_SEED)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="budget of the CPU baseline leg (0 = skip)")
     ap.add_argument("--pmc", default=os.path.join(REPO, "profiles", "pmc_traffic.json"))
@@ -70,12 +84,10 @@ def parse(argv=None):
                          "default shape stripe 0 is also checked against the committed full-size digests)")
     ap.add_argument("--verify", dest="verify", action="store_true")
     ap.add_argument("--hbm-fill", action="store_true",
-                    help="BASELINE configs[3]: 256 stripes, block size = the largest whole MiB at which the "
-                         "batch fits one GPU's free HBM (the N>1 default, split over the ranks)")
+                    help="main leg = BASELINE configs[3]: 256 stripes, block size = the largest whole MiB at which "
+                         "the batch fits one GPU's free HBM (split by stripe over the ranks at N>1)")
     ap.add_argument("--strong", action="store_true",
-                    help="strong scaling: --stripes (or the --hbm-fill batch) is the TOTAL, split by stripe")
-    ap.add_argument("--weak", action="store_true",
-                    help="N>1: every rank runs the N=1 slab (weak scaling) instead of the configs[4] split")
+                    help="strong scaling: --stripes is the TOTAL, split by stripe (default: per GPU)")
     ap.add_argument("--dry-run", action="store_true",
                     help="no GPU: plan every rank's share and run the rank orchestration and timing reduction "
                          "only (CPU test of the N>1 path; --dry-run-free-gib stands in for free HBM)")
@@ -185,14 +197,17 @@ class Dist:
             dist.destroy_process_group()
 
 
-def plan(args, d: Dist, free_bytes: int, parity_num: int) -> dict:
-    """The workload and this rank's share of it (same on every rank except
-    the share). free_bytes: this GPU's free HBM before any allocation."""
+def plan(args, d: Dist, free_bytes: int, parity_num: int, fill: bool = False) -> dict:
+    """A leg's workload and this rank's share of it (the same on every rank
+    except the share). Main leg: args.stripes (default 8) stripes of
+    args.block_mib (default 64) MiB PER GPU (weak scaling), or in total with
+    --strong. fill: the configs[3] batch -- 256 stripes, B = the largest whole
+    MiB at which the WHOLE batch fits one GPU's free HBM (the MIN over ranks,
+    so the same B at every N), split by stripe (strong). free_bytes: this
+    GPU's free HBM (only read for fill)."""
     from ecwide_amd.shard import hbm_fill_block_mib, plan_rank
 
     k = args.k
-    fill = args.hbm_fill or (d.world > 1 and not args.weak and args.stripes is None and args.block_mib is None)
-    strong = args.strong or (fill and d.world > 1 and not args.weak)
     if fill:
         total = HBM_FILL_STRIPES
         # the whole batch fits ONE GPU at this B, so B is the same at every N
@@ -201,10 +216,11 @@ def plan(args, d: Dist, free_bytes: int, parity_num: int) -> dict:
         mib = int(d.reduce(float(mib), "min"))
         if mib < 1:
             raise SystemExit(f"bench.py: {free_bytes} B free: too small for {total} stripes")
-        block_mib = float(mib)
+        block_mib, strong = float(mib), True
     else:
         total = args.stripes if args.stripes is not None else 8
         block_mib = args.block_mib if args.block_mib is not None else 64.0
+        strong = args.strong
     B = int(block_mib * (1 << 20))
     align = (args.chunk_kib << 10) if args.layout == "tiled" else 4096
     share = plan_rank(total, B, d.world, d.rank, strong, per_rank=total, align=align)
@@ -212,6 +228,43 @@ def plan(args, d: Dist, free_bytes: int, parity_num: int) -> dict:
         raise SystemExit("bench.py: more ranks than column tiles")
     stripes_total = total if strong else total * d.world
     return dict(hbm_fill=fill, strong=strong, stripes_total=stripes_total, block_bytes_full=B, share=share)
+
+
+def layout_desc(args) -> str:
+    return {"blocks": "blocks (each block contiguous, block stride B + 4 KiB, [D.., G.., L..] per stripe)",
+            "split": "split (each block contiguous, block stride B + 4 KiB, parity blocks in their own "
+                     "region)"}.get(args.layout, f"tiled ({args.chunk_kib} KiB column pieces: the k data "
+                                                 f"pieces contiguous, parities in their own region)")
+
+
+def workload_of(pl, k, m, r, g, world) -> str:
+    """The workload's description: the same at every N (it names the per-GPU
+    or total amount, never the rank count)."""
+    B, S_total = pl["block_bytes_full"], pl["stripes_total"]
+    if pl["hbm_fill"]:
+        return (f"configs[3]/[4]: {S_total} independent CL(k={k}, r={r}, m={m}, g={g}) stripes of B={B >> 20} MiB "
+                f"blocks (the batch that fills one GPU's HBM, {S_total * (k + m + g) * B / 2**30:.0f} GiB), split "
+                f"by stripe over the GPUs: batched encode + repair of D0")
+    if pl["strong"]:
+        return (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {S_total} stripes in total split by stripe "
+                f"over the GPUs: batched encode + repair of D0")
+    return (f"CL(k={k}, r={r}, m={m}, g={g}) B={B >> 20} MiB, {pl['share']['stripes']} stripes per GPU (weak "
+            f"scaling): batched encode + repair of D0")
+
+
+def config_of(args, pl, k, m, r, g, world, enc_bytes, rep_bytes) -> dict:
+    """The line's `config`: identical at every N apart from stripes_total."""
+    sh = pl["share"]
+    return {
+        "workload": workload_of(pl, k, m, r, g, world),
+        "k": k, "r": r, "m": m, "g": g, "block_bytes": pl["block_bytes_full"],
+        "block_bytes_per_gpu": sh["block_bytes"],
+        "stripes_per_gpu": sh["stripes"], "stripes_total": pl["stripes_total"], "seed": args.seed,
+        "parallelism": "stripes partitioned over the GPUs, one process per GPU (no collectives on the data path)",
+        "layout": layout_desc(args),
+        "encode_bytes_per_step_per_gpu": enc_bytes,
+        "repair_bytes_per_step_per_gpu": rep_bytes,
+    }
 
 
 # ---- CPU baseline (oracle: test infrastructure, never the measured product) --
@@ -334,100 +387,191 @@ def verify(args, slab, out, pl, k, m, r) -> dict:
     return dict(res, ok=True)
 
 
-def other_layouts(args, E, codec, S, B, s0, out, enc_bytes, rep_bytes, dev) -> dict:
-    """Encode / repair rates of the bench workload in whole-block layouts."""
+def other_layouts(args, E, codec, slab, S, B, out, enc_bytes, rep_bytes, dev) -> dict:
+    """Encode / repair rates of the bench workload in whole-block layouts --
+    the split slab (data blocks, then parity blocks: ISA-L's separate data /
+    coding arrays, batched) and pointer tables over separately allocated 64
+    MiB blocks (the reference's per-block pointers, NativeCodec.cc:158-170,
+    one ecw_encode_ptrs_dev launch for all stripes) -- timed INTERLEAVED with
+    the headline tiled slab (T, S, P in every round, equal steps, one
+    process), so the comparison is not confounded by where each allocation
+    landed physically."""
+    import statistics
+
     import torch
 
-    n2 = args.other_layout_steps
-    res = {}
-
-    def timed(run, nbytes):
-        run()
-        torch.cuda.synchronize()
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        for _ in range(n2):
-            run()
-        e1.record()
-        torch.cuda.synchronize()
-        return round(nbytes * n2 / (e0.elapsed_time(e1) * 1e-3) / 1e9, 2)
-
-    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=dev, layout="split")
-    slab.fill_random(seed=args.seed, s0=s0)
-    enc = timed(slab.encode, enc_bytes)
-    rep = timed(lambda: slab.repair(0, out), rep_bytes)
-    res["split"] = {"layout": "split: whole blocks (stride B + 4 KiB), data blocks of all stripes then their "
-                              "parity blocks", "steps": n2, "encode_GBps": enc, "repair_GBps": rep,
-                    "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
-    del slab
-    torch.cuda.empty_cache()
-    # pointer mode: every block its own allocation (data blocks first, then parities)
+    n2, rounds = args.other_layout_steps, args.other_layout_rounds
     k, np_ = codec.encodeDataNum, codec.parityNum
+    split = E.StripeSlab(codec, stripes=S, block_bytes=B, device=dev, layout="split")
+    split.fill_random(seed=args.seed)
     data = [[torch.empty(B, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(k)] for _ in range(S)]
     par = [[torch.empty(B, dtype=torch.uint8, device=f"cuda:{dev}") for _ in range(np_)] for _ in range(S)]
-    gen = torch.Generator(device=f"cuda:{dev}").manual_seed(args.seed)
-    for blocks in data:
-        for blk in blocks:
-            blk.random_(0, 256, generator=gen)
+    for s_ in range(S):
+        src = split.data(s_)
+        for j in range(k):
+            data[s_][j].copy_(src[j])  # the same bytes as the slabs
     batch = E.BlockBatch(codec, data, par)
-    enc = timed(batch.encode, enc_bytes)
     outs = [out[s_ * B:(s_ + 1) * B] for s_ in range(S)]
-    rep = timed(lambda: batch.repair(0, outs), rep_bytes)
-    res["pointer"] = {"layout": f"pointer mode: {S * (k + np_)} separately allocated {B >> 20} MiB blocks, one "
-                                f"ecw_encode_ptrs_dev / ecw_xor_reduce_ptrs_dev launch over the {S} stripes",
-                      "steps": n2, "encode_GBps": enc, "repair_GBps": rep, "encode_frac": round(enc / HBM_PEAK_GBS, 4)}
+    legs = {
+        "tiled": (slab.encode, lambda: slab.repair(0, out)),
+        "split": (split.encode, lambda: split.repair(0, out)),
+        "pointer": (batch.encode, lambda: batch.repair(0, outs)),
+    }
+    for enc, rep in legs.values():  # warm every leg once
+        enc()
+        rep()
+    torch.cuda.synchronize()
+    rates = {name: ([], []) for name in legs}
+    for _ in range(rounds):
+        for name, (enc, rep) in legs.items():
+            e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+            e[0].record()
+            for _ in range(n2):
+                enc()
+            e[1].record()
+            for _ in range(n2):
+                rep()
+            e[2].record()
+            torch.cuda.synchronize()
+            rates[name][0].append(round(enc_bytes * n2 / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9, 1))
+            rates[name][1].append(round(rep_bytes * n2 / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9, 1))
+    # the pointer leg's parities equal the tiled slab's (same bytes in, same code)
+    same = all(torch.equal(par[s_][i], slab.parity(s_)[i]) for s_ in (0, S - 1) for i in (0, np_ - 1))
+    desc = {
+        "tiled": "tiled slab (the headline layout)",
+        "split": "split slab: whole blocks (stride B + 4 KiB), the data blocks of all stripes then their parity "
+                 "blocks (ecw_encode_batch_split_dev)",
+        "pointer": f"pointer tables: {S * (k + np_)} separately allocated {B >> 20} MiB blocks, one "
+                   f"ecw_encode_ptrs_dev / ecw_xor_reduce_ptrs_dev launch over the {S} stripes",
+    }
+    res = {"interleaved": f"{rounds} rounds x (tiled, split, pointer) x {n2} encodes + {n2} repairs, one process"}
+    for name, (en, rp) in rates.items():
+        med = statistics.median(en)
+        res[name] = {"layout": desc[name], "encode_GBps": med, "repair_GBps": statistics.median(rp),
+                     "encode_frac": round(med / HBM_PEAK_GBS, 4), "encode_GBps_rounds": en, "repair_GBps_rounds": rp}
+    res["pointer"]["parity_equals_tiled"] = bool(same)
+    del split, data, par, batch
     return res
 
 
 # ---- the PCIe-inclusive rate --------------------------------------------------
-def host_resident(args):
-    """PCIe-inclusive rate: blocks live in pinned host memory; ecw_encode /
-    ecw_repair pipeline them through HBM with hipMemcpyAsync in and out.
-    Reported separately, never as the bench `value`."""
+PCIE_GEN5_X16_GBPS = 63.0  # per direction: 32 GT/s x 16 lanes x 128/130 / 8
+
+
+def host_resident_leg(args, dev: int, iters: int) -> dict:
+    """PCIe-inclusive rate: one stripe's blocks live in pinned host memory;
+    ecw_encode / ecw_repair pipeline them through HBM with hipMemcpyAsync in
+    and out (8 MiB column slices, 3 HBM slots, H2D / kernel / D2H on three
+    streams). Reported beside `value`, never as it."""
     import numpy as np
     import torch
 
     import ecwide_amd as E
 
-    torch.cuda.set_device(0)
     k, m, r = args.k, args.m, args.r
     B = int((args.block_mib or 64.0) * (1 << 20))
-    codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, device=dev)
     nblk = k + codec.parityNum
     hb = torch.empty(nblk * B, dtype=torch.uint8, pin_memory=not args.pageable)
-    slab = E.StripeSlab(codec, stripes=1, block_bytes=B)
+    slab = E.StripeSlab(codec, stripes=1, block_bytes=B, device=dev)
     slab.fill_random(seed=args.seed)
     for j in range(k):
         hb[j * B:(j + 1) * B].copy_(slab.block(0, j))
+    slab.encode()  # the expected parities, from the device-resident path
+    want = [p.cpu().numpy() for p in slab.parity(0)]
     del slab
     torch.cuda.synchronize()
     views = [hb[i * B:(i + 1) * B].numpy() for i in range(nblk)]
     out = torch.empty(B, dtype=torch.uint8, pin_memory=not args.pageable).numpy()
-    enc_b = nblk * B
-    rep_b = (len(codec.repairSources(0)) + 1) * B
-    codec.encodeData(views[:k], views[k:])
+    nsrc = len(codec.repairSources(0))
+    enc_b, rep_b = nblk * B, (nsrc + 1) * B
+    codec.encodeData(views[:k], views[k:])  # warm
     codec.repairBlock(views, 0, out)
-    it = max(1, args.steps // 4)
     t0 = time.perf_counter()
-    for _ in range(it):
+    for _ in range(iters):
         codec.encodeData(views[:k], views[k:])
     t1 = time.perf_counter()
-    for _ in range(it):
+    for _ in range(iters):
         codec.repairBlock(views, 0, out)
     t2 = time.perf_counter()
-    assert np.array_equal(out, views[0])
-    line = {
-        "metric": ("host-resident encode + single-block-repair GB/s "
-                   + ("(pageable host blocks, e.g. Java direct ByteBuffers)" if args.pageable
-                      else "(pinned host blocks, hipMemcpyAsync in/out)")),
-        "value": round(it * (enc_b + rep_b) / (t2 - t0) / 1e9, 2),
-        "unit": "GB/s", "n_gpus": 1, "iters": it,
-        "encode_GBps": round(it * enc_b / (t1 - t0) / 1e9, 2),
-        "repair_GBps": round(it * rep_b / (t2 - t1) / 1e9, 2),
-        "pcie_bytes_per_encode": (k + codec.parityNum) * B,
-        "config": {"k": k, "r": r, "m": m, "block_bytes": B, "stripes": 1,
-                   "pipeline": "8 MiB column slices, 3 HBM slots, H2D/kernel/D2H on 3 streams"},
+    ok = np.array_equal(out, views[0]) and all(np.array_equal(a, b) for a, b in zip(views[k:], want))
+    h2d = iters * (k * B + nsrc * B) / (t2 - t0) / 1e9  # bytes the pipeline moved host -> device per second
+    return {
+        "GBps": round(iters * (enc_b + rep_b) / (t2 - t0) / 1e9, 2),
+        "encode_GBps": round(iters * enc_b / (t1 - t0) / 1e9, 2),
+        "repair_GBps": round(iters * rep_b / (t2 - t1) / 1e9, 2),
+        "pcie_bytes_per_step": (k + codec.parityNum) * B + (nsrc + 1) * B,
+        "h2d_GBps": round(h2d, 2),
+        "frac_of_pcie_gen5_x16": round(h2d / PCIE_GEN5_X16_GBPS, 4),
+        "iters": iters, "verified": bool(ok),
+        "host_blocks": "pageable" if args.pageable else "pinned",
+        "config": f"CL(k={k}, r={r}, m={m}) one stripe of {B >> 20} MiB blocks in host memory: encodeData + "
+                  f"repair of D0; 8 MiB column slices, 3 HBM slots, H2D / kernel / D2H on three streams",
     }
+
+
+def chunkgen_leg(args) -> dict:
+    """ECWide-C's ChunkGenerator replay (BASELINE configs[0]; the default
+    ECWide-C/config/scheme.ini: CL k=32, groupDataNum=11, m=3, 64 MiB chunks):
+    source blocks in pinned host memory (BufferUnit's direct ByteBuffers),
+    encodeChunks timed exactly where ChunkGenerator.java:126-131 times it
+    (host -> HBM -> host), then generateChunks writes the D/G/L chunk files
+    (FileOp.writeFile) into a temporary directory, timed separately."""
+    import shutil
+    import tempfile
+
+    import numpy as np
+
+    from ecwide_amd.chunk_generator import ChunkGenerator
+    from ecwide_amd.codec import CodingScheme
+
+    import oracle
+
+    scheme = CodingScheme.fromConfigText("codeType = CL\nk = 32\ngroupDataNum = 11\nglobalParityNum = 3\n"
+                                         "chunkSizeBits = 26\n")
+    tmp = tempfile.mkdtemp(prefix="ecw_chunks_")
+    try:
+        gen = ChunkGenerator(scheme, tmp, "prng")  # the reference's bytes: zero L blocks
+        gen.fill_prng(args.seed)
+        gen.encode_chunks()  # warm (first-call staging)
+        ms = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            gen.encode_chunks()
+            ms.append((time.perf_counter() - t0) * 1e3)
+        B, nb = scheme.chunkSize, scheme.k + gen.codec.parityNum
+        # parity of the replay: an 8 KiB window of every global parity vs the oracle
+        W = 8192
+        oc = oracle.Oracle().codec("C", scheme.k, scheme.globalParityNum, scheme.groupDataNum, W)
+        want = oc.encode([np.ascontiguousarray(b[:W]) for b in gen.data], literal=True)
+        ok = all(np.array_equal(gen.parity[i][:W], w) for i, w in enumerate(want))
+        t0 = time.perf_counter()
+        paths = gen.generate_chunks(0)
+        wms = (time.perf_counter() - t0) * 1e3
+        best = min(ms)
+        return {
+            "config": "ChunkGenerator replay, default scheme.ini: CL(k=32, r=11, m=3), 64 MiB chunks, zero L blocks "
+                      "(the reference's bytes), pinned source buffers",
+            "encodeChunks_ms": [round(x, 3) for x in ms],
+            "encodeChunks_GBps": round(nb * B / (best * 1e-3) / 1e9, 2),
+            "generateChunks_ms": round(wms, 1), "chunk_files": len(paths),
+            "generateChunks_GBps": round(nb * B / (wms * 1e-3) / 1e9, 2), "verified": bool(ok),
+        }
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def host_resident(args):
+    """--host-resident: the PCIe-inclusive leg on its own, as a JSON line."""
+    import torch
+
+    torch.cuda.set_device(0)
+    leg = host_resident_leg(args, 0, max(1, args.steps // 4))
+    line = {"metric": ("host-resident encode + single-block-repair GB/s "
+                       + ("(pageable host blocks, e.g. Java direct ByteBuffers)" if args.pageable
+                          else "(pinned host blocks, hipMemcpyAsync in/out)")),
+            "value": leg["GBps"], "unit": "GB/s", "n_gpus": 1}
+    line.update(leg)
     print(json.dumps(line), flush=True)
 
 
@@ -582,25 +726,145 @@ def ecwide_h_sequence(args, shim, orc, ln: int) -> dict:
 
 # ---- the bench ------------------------------------------------------------------
 def dry_run(args, d: Dist):
-    """The N>1 orchestration without a GPU: plans, a stand-in timed region
-    (each rank sleeps a rank-dependent time) and the same reductions."""
-    g = -(-args.k // args.r)
-    pl = plan(args, d, int(args.dry_run_free_gib * (1 << 30)), args.m + g)
+    """The N>1 orchestration without a GPU: both legs' plans, a stand-in timed
+    region (each rank sleeps a rank-dependent time), the same reductions, and
+    the line's `config` built exactly as the real run builds it."""
+    k, m, r = args.k, args.m, args.r
+    g = -(-k // r)
+    free = int(args.dry_run_free_gib * (1 << 30))
+    pl = plan(args, d, free, m + g, fill=args.hbm_fill)
+    sh = pl["share"]
+    enc_bytes = sh["stripes"] * (k + m + g) * sh["block_bytes"]
+    rep_bytes = sh["stripes"] * (min(r, k) + 1) * sh["block_bytes"]
     d.barrier()
     t0 = time.perf_counter()
     time.sleep(0.05 * (1 + d.rank))
     d.barrier()
     el = time.perf_counter() - t0
     el_max = d.reduce(el, "max")
-    shares = [d.gather(float(pl["share"][key])) for key in ("s0", "stripes", "block_bytes", "col_offset")]
+    shares = [d.gather(float(sh[key])) for key in ("s0", "stripes", "block_bytes", "col_offset")]
     per_rank = d.gather(el)
+    c4 = None
+    if args.configs4_steps > 0 and not args.hbm_fill:
+        p4 = plan(args, d, free, m + g, fill=True)
+        c4 = {"stripes_total": p4["stripes_total"], "block_bytes": p4["block_bytes_full"],
+              "shares": [dict(s0=int(a), stripes=int(b)) for a, b in
+                         zip(*[d.gather(float(p4["share"][key])) for key in ("s0", "stripes")])]}
     if d.rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": d.world, "scaling": "strong" if pl["strong"] else "weak",
                           "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
                           "block_bytes": pl["block_bytes_full"], "el_max": el_max, "rank_seconds": per_rank,
+                          "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
+                          "configs4": c4,
                           "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
                                      for a, b, c, o in zip(*shares)]}), flush=True)
     d.close()
+
+
+def device_leg(args, d: Dist, E, pl: dict, k: int, m: int, r: int, steps: int, warmup: int, layout: str) -> dict:
+    """Fill this rank's share of a leg in HBM, time exactly `steps` steps
+    (encode of the slab + repair of D0 of every stripe) between barriers and
+    synchronisations on both sides, then time each kernel with events on the
+    launch stream in a second pass of the same steps (so the timed region
+    carries no event overhead). Returns the slab, the times and the max over
+    ranks."""
+    import torch
+
+    sh = pl["share"]
+    B, S, s0 = sh["block_bytes"], sh["stripes"], sh["s0"]
+    codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, device=d.dev)
+    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=layout,
+                        chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
+    out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{d.dev}")
+    slab.fill_random(seed=args.seed, s0=s0, col_offset=sh["col_offset"])
+    torch.cuda.synchronize()
+    enc_bytes, rep_bytes = slab.encode_bytes(), slab.repair_bytes(0)
+
+    def step(evs=None):
+        if evs is not None:
+            evs[0].record()
+        slab.encode()
+        if evs is not None:
+            evs[1].record()
+        slab.repair(0, out)
+        if evs is not None:
+            evs[2].record()
+
+    for _ in range(warmup):
+        step()
+    torch.cuda.synchronize()
+    # timed region: exactly `steps` steps
+    d.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    d.barrier()
+    el = time.perf_counter() - t0
+    el_max = d.reduce(el, "max")
+    rank_s = d.gather(el)
+    # per-kernel durations: events on the launch stream (torch's current
+    # stream: slab.encode / repair launch on it)
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for i in range(steps):
+        step(evs[i])
+    torch.cuda.synchronize()
+    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
+    rep_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
+    return dict(codec=codec, slab=slab, out=out, enc_bytes=enc_bytes, rep_bytes=rep_bytes, el_max=el_max,
+                rank_s=rank_s, enc_ms=enc_ms, rep_ms=rep_ms,
+                enc_ms_max=d.reduce(enc_ms, "max"), rep_ms_max=d.reduce(rep_ms, "max"))
+
+
+def pmc_traffic(args, k, r, m, B, S, enc_bytes, launches):
+    """PMC-measured HBM bytes of one encode launch (profiles/pmc_traffic.json,
+    written by tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE
+    rocprofv3 passes over this very workload), or None."""
+    if not os.path.exists(args.pmc):
+        return None
+    try:
+        pmc = json.load(open(args.pmc))
+        key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{args.chunk_kib}k", "split": "_split"}.get(args.layout, "")
+        ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
+        return ratio * enc_bytes / launches if ratio else None
+    except Exception:
+        return None
+
+
+def configs4_leg(args, d: Dist, E, k, m, r) -> dict:
+    """configs[4] (configs[3] at N=1): the 256-stripe batch sized to fill ONE
+    GPU's HBM, split by stripe over the ranks, timed the same way."""
+    import torch
+
+    g = -(-k // r)
+    torch.cuda.empty_cache()
+    d.barrier()  # every rank has freed the main leg before free HBM is read
+    pl = plan(args, d, torch.cuda.mem_get_info(d.dev)[0], m + g, fill=True)
+    leg = device_leg(args, d, E, pl, k, m, r, args.configs4_steps, 1, args.layout)
+    vres = verify(args, leg["slab"], leg["out"], pl, k, m, r)
+    ok = d.reduce(1.0 if vres["ok"] else 0.0, "min") > 0.5
+    sh, S_total = pl["share"], pl["stripes_total"]
+    total_bytes = (leg["enc_bytes"] + leg["rep_bytes"]) * S_total // sh["stripes"] * args.configs4_steps
+    launches = leg["slab"].encode_launches()
+    res = {
+        "baseline_config": "configs[4]" if d.world > 1 else "configs[3]",
+        "workload": workload_of(pl, k, m, r, g, d.world),
+        "value": round(total_bytes / leg["el_max"] / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(leg["el_max"] / args.configs4_steps * 1e3, 4), "steps": args.configs4_steps,
+        "scaling": "strong", "stripes_total": S_total, "stripes_per_gpu": sh["stripes"],
+        "block_bytes": pl["block_bytes_full"],
+        "rank_ms_per_step": [round(x / args.configs4_steps * 1e3, 4) for x in leg["rank_s"]],
+        "encode_GBps": round(leg["enc_bytes"] / (leg["enc_ms_max"] * 1e-3) / 1e9, 2),
+        "repair_GBps": round(leg["rep_bytes"] / (leg["rep_ms_max"] * 1e-3) / 1e9, 2),
+        "encode_frac": round(leg["enc_bytes"] / (leg["enc_ms_max"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+        "encode_launch_ms": round(leg["enc_ms_max"] / launches, 4), "launches_per_encode": launches,
+        "verified": bool(ok),
+        "verify": {key: vres[key] for key in ("windows", "repairs")} | ({"failed": vres["failed"]} if not vres["ok"] else {}),
+    }
+    del leg
+    torch.cuda.empty_cache()
+    return res
 
 
 def main():
@@ -626,94 +890,26 @@ def main():
     import ecwide_amd as E
 
     k, m, r = args.k, args.m, args.r
-    g0 = -(-k // r)
-    pl = plan(args, d, torch.cuda.mem_get_info(d.dev)[0], m + g0)
+    g = -(-k // r)
+    pl = plan(args, d, torch.cuda.mem_get_info(d.dev)[0], m + g, fill=args.hbm_fill)
+    leg = device_leg(args, d, E, pl, k, m, r, args.steps, args.warmup, args.layout)
+    codec, slab, out = leg["codec"], leg["slab"], leg["out"]
+    enc_bytes, rep_bytes = leg["enc_bytes"], leg["rep_bytes"]
     sh = pl["share"]
-    B, S, s0 = sh["block_bytes"], sh["stripes"], sh["s0"]
-    B_full, S_total, columns = pl["block_bytes_full"], pl["stripes_total"], sh["columns"]
-    scheme = E.CodingScheme.getClScheme(k, m, r, B)
-    codec = E.NativeCodec.getClCodec(scheme, 1, False, device=d.dev)
-    slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=args.layout,
-                        chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
-    out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{d.dev}")
-    slab.fill_random(seed=args.seed, s0=s0, col_offset=sh["col_offset"])
-    torch.cuda.synchronize()
-    enc_bytes = slab.encode_bytes()
-    rep_bytes = slab.repair_bytes(0)
-    step_bytes = enc_bytes + rep_bytes
-
-    def step(evs=None):
-        if evs is not None:
-            evs[0].record()
-        slab.encode()
-        if evs is not None:
-            evs[1].record()
-        slab.repair(0, out)
-        if evs is not None:
-            evs[2].record()
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-
-    # timed region: exactly K steps
-    d.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    d.barrier()
-    el = time.perf_counter() - t0
-    el_max = d.reduce(el, "max")
-    rank_s = d.gather(el)
-
-    # per-kernel durations with events on the launch stream (torch's current
-    # stream: slab.encode/repair launch on it) in a separate pass of the same
-    # work, so the timed region carries no event overhead
-    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-    for i in range(args.steps):
-        step(evs[i])
-    torch.cuda.synchronize()
-    enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / args.steps
-    rep_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / args.steps
-
+    B, S = sh["block_bytes"], sh["stripes"]
     vres = None
     if args.verify:
         vres = verify(args, slab, out, pl, k, m, r)
         ok_all = d.reduce(1.0 if vres["ok"] else 0.0, "min") > 0.5
-    if d.rank != 0:
-        d.close()
-        return
-
     # every stripe costs the same bytes; in column mode each stripe's bytes are
     # spread over the ranks in proportion to their column slices
-    total_bytes = step_bytes * B_full // B // S * S_total * args.steps
-    value = total_bytes / el_max / 1e9
-    achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+    total_bytes = (enc_bytes + rep_bytes) * pl["block_bytes_full"] // B // S * pl["stripes_total"] * args.steps
+    value = total_bytes / leg["el_max"] / 1e9
     launches = slab.encode_launches()  # one encode() = `launches` equal kernel launches
-    traffic = None
-    if os.path.exists(args.pmc):
-        try:
-            pmc = json.load(open(args.pmc))
-            key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{args.chunk_kib}k", "split": "_split"}.get(args.layout, "")
-            ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
-            traffic = ratio * enc_bytes / launches if ratio else None  # PMC bytes of one launch
-        except Exception:
-            traffic = None
-    g = codec.groupNum
-    if pl["hbm_fill"]:
-        wl = (f"configs[{4 if d.world > 1 else 3}]: {S_total} independent CL(k={k}, r={r}, m={m}, g={g}) stripes "
-              f"of B={B_full >> 20} MiB blocks (the batch that fills one GPU's HBM, "
-              f"{S_total * (k + m + g) * B_full / 2**30:.0f} GiB)"
-              + (f", split by stripe over {d.world} GPUs: {S} on rank 0" if d.world > 1 else "")
-              + ": batched encode + repair of D0")
-    else:
-        wl = (f"CL(k={k}, r={r}, m={m}, g={g}) B={B_full >> 20} MiB, "
-              + (f"{S_total} stripes in total" if pl["strong"] else f"{S} stripes/GPU")
-              + ": batched encode + repair of D0")
-    if columns:
-        wl += f" [column-sliced: {B} of {B_full} B per block on rank 0]"
+    # the slowest rank's kernel times: a per-GPU roofline that holds for every GPU
+    enc_ms, rep_ms = leg["enc_ms_max"], leg["rep_ms_max"]
+    achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(args, k, r, m, B, S, enc_bytes, launches)
     line = {
         "metric": "device-resident encode + single-block-repair GB/s, wide stripe (shards in HBM)",
         "value": round(value, 2),
@@ -721,27 +917,16 @@ def main():
         "n_gpus": d.world,
         "steps": args.steps,
         "warmup": args.warmup,
-        "ms_per_step": round(el_max / args.steps * 1e3, 4),
+        "ms_per_step": round(leg["el_max"] / args.steps * 1e3, 4),
         "higher_is_better": True,
         "scaling": "strong" if pl["strong"] else "weak",
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic (counter PRNG of include/ecwide.h, uniform random bytes, generated in HBM)",
-        "config": {
-            "workload": wl,
-            "k": k, "r": r, "m": m, "g": g, "block_bytes": B_full, "block_bytes_per_gpu": B,
-            "stripes_per_gpu": S, "stripes_total": S_total, "seed": args.seed,
-            "parallelism": f"stripe-partitioned x{d.world} (no collectives on the data path)",
-            "layout": {"blocks": "blocks (each block contiguous, block stride B + 4 KiB, [D.., G.., L..] per stripe)",
-                       "split": "split (each block contiguous, block stride B + 4 KiB, parity blocks in their own "
-                                "region)"}.get(args.layout, f"tiled ({args.chunk_kib} KiB column pieces: the k data "
-                                                            f"pieces contiguous, parities in their own region)"),
-            "encode_bytes_per_step_per_gpu": enc_bytes,
-            "repair_bytes_per_step_per_gpu": rep_bytes,
-        },
-        "rank_ms_per_step": [round(x / args.steps * 1e3, 4) for x in rank_s],
+        "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
+        "rank_ms_per_step": [round(x / args.steps * 1e3, 4) for x in leg["rank_s"]],
         "devices_distinct": d.distinct,
-        "encode_GBps": round(enc_bytes / (enc_ms * 1e-3) / 1e9, 2),
+        "encode_GBps": round(achieved, 2),
         "repair_GBps": round(rep_bytes / (rep_ms * 1e-3) / 1e9, 2),
         "roofline": {
             "bound": "hbm",
@@ -751,6 +936,7 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "per_gpu": "the slowest rank's launch time" if d.world > 1 else "one GPU",
             # PMC-measured HBM bytes of one launch over this run's launch time
             "traffic_GBps": round(traffic * launches / (enc_ms * 1e-3) / 1e9, 2) if traffic else None,
             # per kernel launch (rocprof's unit); one encode() of the slab = `launches` launches
@@ -767,18 +953,19 @@ def main():
         line["verified"] = bool(ok_all)
         line["verify"] = {key: vres[key] for key in ("windows", "repairs", "digests")} | (
             {"failed": vres["failed"]} if not vres["ok"] else {})
-    if d.world == 1 and args.other_layout_steps > 0 and not pl["hbm_fill"]:
-        # the same workload with whole contiguous blocks (not `value`): the split
-        # slab (data blocks, then parity blocks, ecw_*_batch_split_dev) and the
-        # reference's per-block pointer interface on separately allocated blocks
-        # (one ecw_encode_ptrs_dev launch for all stripes)
-        del slab
-        torch.cuda.empty_cache()
-        line["other_layout"] = other_layouts(args, E, codec, S, B, s0, out, enc_bytes, rep_bytes, d.dev)
-        torch.cuda.empty_cache()
-    if d.world == 1 and args.cpu_seconds > 0:
-        line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)
-    print(json.dumps(line), flush=True)
+    if d.world == 1 and args.other_layout_steps > 0 and args.other_layout_rounds > 0 and not pl["hbm_fill"]:
+        line["other_layout"] = other_layouts(args, E, codec, slab, S, B, out, enc_bytes, rep_bytes, d.dev)
+    del leg, slab, out, codec
+    torch.cuda.empty_cache()
+    if args.configs4_steps > 0 and not pl["hbm_fill"]:
+        line["configs4"] = configs4_leg(args, d, E, k, m, r)
+    if d.rank == 0:
+        if args.cpu_seconds > 0:
+            line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)
+        if args.host_iters > 0:
+            line["host_resident"] = host_resident_leg(args, d.dev, args.host_iters)
+            line["host_resident"]["chunk_generator"] = chunkgen_leg(args)
+        print(json.dumps(line), flush=True)
     d.close()
 
 

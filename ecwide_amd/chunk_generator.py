@@ -8,6 +8,12 @@ chunk files with the reference's names. This is BASELINE config #1
     python -m ecwide_amd.chunk_generator [zero|urandom|prng] [toy|<stripes>] \
         [--scheme config/scheme.ini] [--settings config/settings.ini] [--chunks-dir DIR]
 
+The chunk files hold the reference's bytes by default: ECWide-C's
+encodeData writes all-zero local parities (NativeCodec.cc:181-186: the XOR
+table is built from a zeroed matrix), and so does this replay, like the JNI
+drop-in libcodec.so; ``--xor`` writes the CL code as designed (L = XOR of the
+group, what decodeData's repair assumes).
+
 Differences, deliberate: ChunkGenerator.main parses args[0] (the source) as
 the stripe count when args[1] != "toy" (ChunkGenerator.java:118-119), which
 throws; here args[1] is the count. "prng" (the ecwide.h counter generator)
@@ -63,7 +69,7 @@ def chunk_file_names(scheme, stripe_id: int) -> list:
 
 
 class ChunkGenerator:
-    def __init__(self, scheme, dir_name: str, source: str, local_mode: str = "xor", pinned: bool = True):
+    def __init__(self, scheme, dir_name: str, source: str, local_mode: str = "literal", pinned: bool = True):
         from .codec import NativeCodec
 
         self.scheme = scheme
@@ -139,12 +145,13 @@ def main(argv=None) -> int:
     ap.add_argument("--settings", default="config/settings.ini")
     ap.add_argument("--chunks-dir", default=None)
     ap.add_argument("--seed", type=int, default=1)
-    ap.add_argument("--literal", action="store_true", help="ECWide-C's all-zero local parities")
+    ap.add_argument("--xor", action="store_true",
+                    help="XOR local parities (the CL code as designed) instead of ECWide-C's all-zero L blocks")
     a = ap.parse_args(argv)
     gen_num = -1 if a.mode == "toy" else int(a.mode)
     chunks_dir = a.chunks_dir or read_settings(a.settings)["chunksDir"]
     scheme = CodingScheme.getFromConfig(a.scheme)
-    gen = ChunkGenerator(scheme, chunks_dir, a.source, local_mode="literal" if a.literal else "xor")
+    gen = ChunkGenerator(scheme, chunks_dir, a.source, local_mode="xor" if a.xor else "literal")
     print("create ChunkGenerator OK")
     if a.source == "prng":
         gen.fill_prng(a.seed)

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cctype>
 #include <chrono>
 #include <condition_variable>
@@ -53,11 +54,89 @@ int status_of(hipError_t e) { return e == hipSuccess ? ECW_OK : ECW_EDEVICE; }
 
 }  // namespace
 
+namespace svc {
+bool busy(int device);  // the request service's resident kernel is (or may be) running on `device`
+}  // namespace svc
+
+// ---- deferred release of device resources -----------------------------------
+// hipFree / hipHostFree / hipStreamDestroy can wait for the device to go idle,
+// which it does not while the request service's resident kernel serves other
+// threads (up to its lifetime). Codec teardown and staging growth therefore
+// hand their old allocations to this list while the service runs; they are
+// released by the first codec create / destroy / staging growth that finds
+// the service gone, and at process exit.
+namespace grave {
+
+enum Kind { kDevice, kHost, kStream, kEvent };
+struct Item {
+  void* p;
+  Kind kind;
+  int device;
+};
+std::mutex mu;
+std::vector<Item> items;
+
+void release_now(const Item& it) {
+  DeviceGuard g(it.device);
+  switch (it.kind) {
+    case kDevice: (void)hipFree(it.p); break;
+    case kHost: (void)hipHostFree(it.p); break;
+    case kStream: (void)hipStreamDestroy(static_cast<hipStream_t>(it.p)); break;
+    case kEvent: (void)hipEventDestroy(static_cast<hipEvent_t>(it.p)); break;
+  }
+}
+
+// release everything of devices whose service is not running
+void reap() {
+  std::vector<Item> now;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if (items.empty()) return;
+    std::vector<Item> keep;
+    for (const Item& it : items) (svc::busy(it.device) ? keep : now).push_back(it);
+    items.swap(keep);
+  }
+  for (const Item& it : now) release_now(it);
+}
+
+// release `p` now, or later if the service on its device is running
+void release(void* p, Kind kind, int device) {
+  if (!p) return;
+  if (svc::busy(device)) {
+    std::lock_guard<std::mutex> lk(mu);
+    items.push_back(Item{p, kind, device});
+    return;
+  }
+  release_now(Item{p, kind, device});
+  reap();
+}
+
+}  // namespace grave
+
+// Ticket counters of ticket-ordered encode launches: a ring of 8-byte device
+// counters, one per launch. The host zeroes the slot's counter on the launch's
+// stream right before the launch and records an event after it; a slot is
+// reused only once that event has completed (the host waits for it in the rare
+// case that kTicketSlots launches later it has not). So no two launches share
+// a counter whatever their streams are (hipStreamPerThread from several
+// threads, a destroyed stream's handle reused, ...). Launches on a capturing
+// stream take the launch windows instead (no counter in a graph).
+constexpr int kTicketSlots = 64;
+struct TicketRing {
+  unsigned long long* d = nullptr;
+  hipEvent_t ev[kTicketSlots] = {};
+  bool used[kTicketSlots] = {};
+  unsigned next = 0;
+};
+
+std::atomic<unsigned long long> g_codec_serial{0};
+
 struct ecw_codec {
   ecw_scheme scheme{};
   ecw_codec_info info{};
   int device = 0;
   int xori_mode = ECW_XORI_XOR;
+  unsigned long long serial = ++g_codec_serial;  // unique per codec (the service's LDS table cache key)
   std::vector<uint8_t> matrix;        // m x edn, row-major (encodeMatrix)
   std::vector<uint8_t> gftbl;         // 32 * edn * m (encodeGftbl, ISA-L layout)
   std::vector<uint8_t> dtbl, pdtbl;   // decode / partial-decode tables (all ones)
@@ -76,21 +155,19 @@ struct ecw_codec {
   uint8_t* h_stage = nullptr;         // pinned host staging of the small-block path
   size_t h_stage_bytes = 0;
 
-  // ticket counters of big encodes, one per stream (ecw_internal.hpp
-  // TicketCounter); ticket_mu serialises the launches that use them
-  std::mutex ticket_mu;
-  std::map<hipStream_t, TicketCounter> tickets;
+  std::mutex ticket_mu;               // guards `tickets`
+  TicketRing tickets;
 
   ~ecw_codec() {
-    if (dev_ready || !d_pass.empty() || !tickets.empty()) {
-      DeviceGuard g(device);
-      for (auto& kv : tickets) (void)hipFree(kv.second.ptr);
-      for (void* p : d_pass) (void)hipFree(p);
-      if (d_stage) (void)hipFree(d_stage);
-      if (h_stage) (void)hipHostFree(h_stage);
-      if (stream) (void)hipStreamDestroy(stream);
-      destroy_pipe();
-    }
+    // every allocation goes through grave::release: freed now, or once the
+    // request service on this device has left (a destroy never waits for it)
+    for (int i = 0; i < kTicketSlots; ++i) grave::release(tickets.ev[i], grave::kEvent, device);
+    grave::release(tickets.d, grave::kDevice, device);
+    for (void* p : d_pass) grave::release(p, grave::kDevice, device);
+    grave::release(d_stage, grave::kDevice, device);
+    grave::release(h_stage, grave::kHost, device);
+    grave::release(stream, grave::kStream, device);
+    destroy_pipe();
   }
   void destroy_pipe();
 
@@ -107,7 +184,7 @@ struct ecw_codec {
     DeviceGuard g(device);
     if (!g.ok) return ECW_EDEVICE;
     auto fail = [&](int st) {  // leave nothing half-initialised: a later call retries from scratch
-      for (void* q : d_pass) (void)hipFree(q);
+      for (void* q : d_pass) grave::release(q, grave::kDevice, device);
       d_pass.clear();
       return st;
     };
@@ -122,30 +199,56 @@ struct ecw_codec {
     return ECW_OK;
   }
 
-  // the counter of stream s (caller holds ticket_mu); null when it cannot be
-  // allocated: the encode then runs in launch windows
-  TicketCounter* ticket_for(hipStream_t s) {
-    auto it = tickets.find(s);
-    if (it != tickets.end()) return &it->second;
-    void* p = nullptr;
-    if (hipMalloc(&p, sizeof(unsigned long long)) != hipSuccess) {
+  // A zeroed counter for one ticket-ordered launch on stream s (caller holds
+  // ticket_mu and calls ticket_done after the launch), or null: the encode
+  // then runs in launch windows.
+  unsigned long long* ticket_take(hipStream_t s, int* slot) {
+    *slot = -1;
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &cap) != hipSuccess || cap != hipStreamCaptureStatusNone) {
       (void)hipGetLastError();
       return nullptr;
     }
-    if (hipMemsetAsync(p, 0, sizeof(unsigned long long), s) != hipSuccess) {
+    TicketRing& t = tickets;
+    if (!t.d) {
+      void* p = nullptr;
+      if (hipMalloc(&p, sizeof(unsigned long long) * kTicketSlots) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+      }
+      t.d = static_cast<unsigned long long*>(p);
+    }
+    const int i = static_cast<int>(t.next++ % kTicketSlots);
+    if (!t.ev[i] && hipEventCreateWithFlags(&t.ev[i], hipEventDisableTiming) != hipSuccess) {
+      t.ev[i] = nullptr;
       (void)hipGetLastError();
-      (void)hipFree(p);
       return nullptr;
     }
-    TicketCounter& t = tickets[s];
-    t.ptr = static_cast<unsigned long long*>(p);
-    t.next = 0;
-    return &t;
+    if (t.used[i] && hipEventSynchronize(t.ev[i]) != hipSuccess) {  // launched kTicketSlots ago and still running
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    t.used[i] = false;
+    if (hipMemsetAsync(t.d + i, 0, sizeof(unsigned long long), s) != hipSuccess) {
+      (void)hipGetLastError();
+      return nullptr;
+    }
+    *slot = i;
+    return t.d + i;
+  }
+  void ticket_done(int slot, hipStream_t s) {
+    if (slot < 0) return;
+    if (hipEventRecord(tickets.ev[slot], s) == hipSuccess) {
+      tickets.used[slot] = true;
+    } else {  // no event to wait for: make sure the launch is over before the slot is reused
+      (void)hipGetLastError();
+      (void)hipStreamSynchronize(s);
+    }
   }
 
   int ensure_stage(size_t bytes) {
     if (stage_bytes >= bytes) return ECW_OK;
-    if (d_stage) (void)hipFree(d_stage);
+    grave::release(d_stage, grave::kDevice, device);
     d_stage = nullptr;
     stage_bytes = 0;
     if (hipMalloc(&d_stage, bytes) != hipSuccess) return ECW_ENOMEM;
@@ -154,7 +257,7 @@ struct ecw_codec {
   }
   int ensure_host_stage(size_t bytes) {
     if (h_stage_bytes >= bytes) return ECW_OK;
-    if (h_stage) (void)hipHostFree(h_stage);
+    grave::release(h_stage, grave::kHost, device);
     h_stage = nullptr;
     h_stage_bytes = 0;
     // coherent: the zero-copy path (encode_stripes_packed) has kernels read and
@@ -230,7 +333,10 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
     if (t.slab) {
       if (encode_uses_ticket(g.tiles * static_cast<uint64_t>(t.stripes), k)) {
         std::lock_guard<std::mutex> lk(c->ticket_mu);
-        e = launch_encode_slab(*t.slab, g, c->d_pass[q], s, c->ticket_for(s));
+        int slot;
+        unsigned long long* tk = c->ticket_take(s, &slot);
+        e = launch_encode_slab(*t.slab, g, c->d_pass[q], s, tk);
+        c->ticket_done(slot, s);
       } else {
         e = launch_encode_slab(*t.slab, g, c->d_pass[q], s, nullptr);
       }
@@ -243,7 +349,10 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
         for (int i = 0; i < ng; ++i) rows.dst[g.nrows + i] = t.dst[m + i];
       if (encode_uses_ticket(g.tiles, k)) {
         std::lock_guard<std::mutex> lk(c->ticket_mu);
-        e = launch_encode_ptr(rows, g, c->d_pass[q], s, c->ticket_for(s));
+        int slot;
+        unsigned long long* tk = c->ticket_take(s, &slot);
+        e = launch_encode_ptr(rows, g, c->d_pass[q], s, tk);
+        c->ticket_done(slot, s);
       } else {
         e = launch_encode_ptr(rows, g, c->d_pass[q], s, nullptr);
       }
@@ -512,7 +621,10 @@ int ecw_codec_create(const ecw_scheme* sch, int node_index, int multinode, int l
   return ECW_OK;
 }
 
-void ecw_codec_destroy(ecw_codec* codec) { delete codec; }
+void ecw_codec_destroy(ecw_codec* codec) {
+  delete codec;
+  grave::reap();  // what earlier teardowns deferred, if the service has left since
+}
 
 int ecw_matrix_codec_create(const uint8_t* matrix, int k, int rows, int device, ecw_codec** out) {
   if (!matrix || !out || k < 1 || rows < 1 || k > kMaxSrc || rows > 255) return ECW_EINVAL;
@@ -627,7 +739,10 @@ int ecw_encode_ptrs_dev(ecw_codec* c, int stripes, const uint8_t* const* d_data_
     hipError_t e;
     if (encode_uses_ticket(eg.tiles * static_cast<uint64_t>(stripes), k)) {
       std::lock_guard<std::mutex> lk(c->ticket_mu);
-      e = launch_encode_tab(rows, eg, c->d_pass[q], s, c->ticket_for(s));
+      int slot;
+      unsigned long long* tk = c->ticket_take(s, &slot);
+      e = launch_encode_tab(rows, eg, c->d_pass[q], s, tk);
+      c->ticket_done(slot, s);
     } else {
       e = launch_encode_tab(rows, eg, c->d_pass[q], s, nullptr);
     }
@@ -883,12 +998,10 @@ struct HostPipe {
     ok = true;
     return ECW_OK;
   }
-  void destroy() {
-    for (hipStream_t st : {s_in, s_run, s_out})
-      if (st) (void)hipStreamDestroy(st);
+  void destroy(int device) {
+    for (hipStream_t st : {s_in, s_run, s_out}) grave::release(st, grave::kStream, device);
     for (int i = 0; i < kSlots; ++i)
-      for (hipEvent_t e : {ev_in[i], ev_run[i], ev_out[i]})
-        if (e) (void)hipEventDestroy(e);
+      for (hipEvent_t e : {ev_in[i], ev_run[i], ev_out[i]}) grave::release(e, grave::kEvent, device);
   }
 };
 
@@ -950,7 +1063,7 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
 
 void ecw_codec::destroy_pipe() {
   if (pipe) {
-    pipe->destroy();
+    pipe->destroy(device);
     delete pipe;
     pipe = nullptr;
   }
@@ -1014,8 +1127,14 @@ struct Service {
       return ECW_EDEVICE;
     const char* e = std::getenv("ECW_SERVICE_IDLE_MS");
     const unsigned long long idle_ms = e ? std::strtoull(e, nullptr, 10) : 20;
+    // A lifetime bounds how long the resident kernel holds the device while
+    // callers keep it busy: device-wide synchronisation (hipDeviceSynchronize,
+    // hipFree) and other kernels sharing its hardware queue wait for it to
+    // leave. 100 ms costs a relaunch (~10 us) per 100 ms of service.
+    const char* l = std::getenv("ECW_SERVICE_LIFE_MS");
+    const unsigned long long life_ms = l ? std::strtoull(l, nullptr, 10) : 100;
     idle_ticks = idle_ms * static_cast<unsigned long long>(khz);
-    life_ticks = 2000ull * static_cast<unsigned long long>(khz);
+    life_ticks = (life_ms ? life_ms : 1) * static_cast<unsigned long long>(khz);
     void* h = nullptr;
     if (hipHostMalloc(&h, sizeof(SvcCtl), hipHostMallocCoherent | hipHostMallocMapped) != hipSuccess)
       return ECW_ENOMEM;
@@ -1079,6 +1198,20 @@ struct Service {
 
 std::mutex g_mu;
 std::map<int, Service*> g_services;  // one per device, kept for the life of the process
+
+// (declared at the top) the resident kernel has been launched and has not
+// published its exit yet
+extern "C++" bool busy(int device) {
+  Service* sv;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    auto it = g_services.find(device);
+    if (it == g_services.end()) return false;
+    sv = it->second;
+  }
+  std::lock_guard<std::mutex> lk(sv->mu);
+  return sv->ctl && sv->epoch != 0 && __atomic_load_n(&sv->ctl->exited_epoch, __ATOMIC_ACQUIRE) != sv->epoch;
+}
 
 #ifndef ECW_SVC_TRACE
 #define ECW_SVC_TRACE 0  // tools only (tools/variants.py): per-phase latency of served calls, printed at exit
@@ -1188,6 +1321,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     w.local_mode = local_mode_of(c);
     w.nw = nw;
     w.flags = c->xor_row ? kSvcXorRow : 0;
+    w.serial = c->serial;
     return w;
   }();
   unsigned long long gen = q.seq >> kSvcSeqBits;
@@ -1210,6 +1344,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
   if (!up) return release(kNotServed);
   const auto t0 = std::chrono::steady_clock::now();
   int failed = ECW_OK;
+  bool timed_out = false;
   // every part with work publishes its own done word (one cache line)
   auto finished = [&] {
     for (int p = 0; p < active; ++p)
@@ -1224,14 +1359,24 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     std::lock_guard<std::mutex> lk(sv->mu);
     if (finished()) break;
     // the epoch this request was posted to left before serving it: start the next one
-    if (sv->ensure_running() != ECW_OK ||
-        std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {  // 10 s: the device is gone
+    if (sv->ensure_running() != ECW_OK) {  // a HIP error: the launch path takes this call and every later one
       sv->broken = true;
       failed = ECW_EDEVICE;
       break;
     }
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
+      // Not served in 10 s. An epoch that has not started is queued behind
+      // other work on the device (contention): this call takes the launch path
+      // (the slot is given back; a late serve only rewrites its own staging).
+      // An epoch that runs and does not serve is broken: the launch path takes
+      // every later call too.
+      if (__atomic_load_n(&sv->ctl->started_epoch, __ATOMIC_ACQUIRE) == sv->epoch) sv->broken = true;
+      timed_out = true;
+      break;
+    }
   }
   if (failed) return release(failed);
+  if (timed_out) return release(kNotServed);
 #if ECW_SVC_TRACE
   const auto tr2 = std::chrono::steady_clock::now();
 #endif

@@ -52,6 +52,30 @@ struct PtrTabRows {
   int np;
 };
 
+// u32 division by a divisor fixed for a launch (Granlund-Montgomery, the
+// round-down-and-fix-up form): q = fast_div(n, f) == n / f.d for every n < 2^32.
+// The kernels map a tile index to (stripe, column tile) with it in a handful of
+// scalar instructions; a 64-bit division by a kernel argument compiled to ~100
+// instructions per tile whose hoisted reciprocals the encode kernel had to
+// spill to scratch (and reload, behind vmcnt(0), at every tile).
+struct FastDiv {
+  uint32_t d, m, s1, s2;
+};
+inline FastDiv make_fastdiv(uint32_t d) {
+  uint32_t l = 0;
+  while (l < 32 && (uint64_t(1) << l) < d) ++l;  // l = ceil(log2 d)
+  FastDiv f;
+  f.d = d;
+  f.m = static_cast<uint32_t>(((uint64_t(1) << 32) * ((uint64_t(1) << l) - d)) / d + 1);
+  f.s1 = l < 1 ? l : 1;
+  f.s2 = l > 1 ? l - 1 : 0;
+  return f;
+}
+__host__ __device__ inline uint32_t fast_div(uint32_t n, const FastDiv& f) {
+  const uint32_t t = static_cast<uint32_t>((static_cast<uint64_t>(n) * f.m) >> 32);
+  return (t + ((n - t) >> f.s1)) >> f.s2;
+}
+
 struct EncodeGeom {
   uint64_t len;          // bytes per block
   uint64_t tiles;        // column tiles per stripe = ceil(len / kTileBytes)
@@ -60,33 +84,25 @@ struct EncodeGeom {
   int m;                 // total global rows (slab output indexing)
   int row0, nrows;       // global rows of this pass [row0, row0 + nrows)
   int local_mode;        // LocalMode
-  uint64_t tile_begin;   // this launch covers slab tiles [tile_begin, tile_end)
-  uint64_t tile_end;     //   (tile = stripe * tiles + column tile)
-  unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter
-  uint64_t ticket_base;        //   whose value at this launch's start is ticket_base
+  // set by the launcher:
+  uint32_t tile_begin;   // this launch covers tiles [tile_begin, tile_end) of its numbering:
+  uint32_t tile_end;     //   tile = stripe * per.d + column tile (the asm kernel numbers full tiles only)
+  FastDiv per;           // column tiles per stripe in that numbering
+  unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter (zeroed before the launch)
   uint32_t wmask, wwidth;      // write window (asm tile): store when (clock & wmask) < wwidth; 0 = off
-};
-
-// Device counter of ticket-ordered encode launches, one per (codec, stream).
-// It is never reset: a launch whose grid has G workgroups over T tiles takes
-// exactly T + G tickets (every workgroup draws one past the end to stop), so
-// the host knows the counter's value at the start of the next launch on the
-// same stream. The owner serialises launches that use one counter.
-struct TicketCounter {
-  unsigned long long* ptr = nullptr;
-  uint64_t next = 0;
 };
 
 // Launchers return hipSuccess or the launch error (an earlier, unrelated HIP
 // error of the calling thread is cleared first, not reported). The encode
 // launchers run a slab of >= ECW_TICKET_MIN_TILES tiles as one ticket-ordered
-// launch when `tc` is given, else in launch windows.
+// launch when `ticket` is given (an 8-byte device counter the caller has
+// zeroed on stream `s` and keeps for this launch alone), else in launch windows.
 hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl,
-                             hipStream_t s, TicketCounter* tc);
+                             hipStream_t s, unsigned long long* ticket);
 hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl,
-                              hipStream_t s, TicketCounter* tc);
+                              hipStream_t s, unsigned long long* ticket);
 hipError_t launch_encode_tab(const PtrTabRows& rows, const EncodeGeom& g, const void* d_tbl,
-                             hipStream_t s, TicketCounter* tc);
+                             hipStream_t s, unsigned long long* ticket);
 // true when an encode of `tiles` column tiles at k data rows would use a ticket counter
 bool encode_uses_ticket(uint64_t tiles, int k);
 
@@ -134,6 +150,11 @@ hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, 
                               uint64_t offset, uint64_t seed, int s0, int b0, hipStream_t s);
 
 int device_cu_count(int device);
+
+// Stripes one launch may cover when each has `tiles` column tiles: the
+// kernels number tiles in 32 bits, so a launch covers fewer than 2^31 tiles
+// and a larger batch goes in several launches over consecutive stripes.
+int stripes_per_launch(uint64_t tiles);
 
 // ---- small-stripe request service (ecw_codec.cpp: svc::) -------------------
 // A resident kernel serves synchronous small encodes (ECWide-H encodes one
@@ -188,6 +209,7 @@ struct alignas(64) SvcSlot {
   uint8_t* data;             // k input rows, `cs` bytes apart (device view of pinned staging)
   uint8_t* out;              // parity rows [G.., L..], `cs` bytes apart
   unsigned long long len, cs;
+  unsigned long long serial;  // the codec's unique serial: tables staged in LDS are its tables
   int k, nrows, m, r, groups, local_mode, nw, flags;  // flags: kSvcXorRow
   unsigned long long trace[8];  // tools only (ECW_SVC_TRACE): phase stamps of the last part
 };
@@ -195,7 +217,8 @@ struct alignas(64) SvcSlot {
 struct SvcCtl {
   unsigned long long stop;          // host: leave now
   unsigned long long exited_epoch;  // device: the epoch that last left the loop
-  unsigned long long pad[6];
+  unsigned long long started_epoch; // device: the epoch whose first workgroup is running
+  unsigned long long pad[5];
   SvcSlot slot[kSvcSlots];
 };
 

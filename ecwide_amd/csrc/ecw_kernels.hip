@@ -242,10 +242,10 @@ struct TileAt {
   bool full;
 };
 
-__device__ __forceinline__ TileAt tile_at(const EncodeGeom& g, uint64_t tile) {
-  const int s = static_cast<int>(tile / g.tiles);
-  const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
-  return {s, col0 + threadIdx.x * kLaneBytes, static_cast<uint64_t>(col0) + kTileBytes <= g.len};
+__device__ __forceinline__ TileAt tile_at(const EncodeGeom& g, uint32_t tile) {
+  const uint32_t s = fast_div(tile, g.per);
+  const uint32_t col0 = (tile - s * g.per.d) * kTileBytes;
+  return {static_cast<int>(s), col0 + threadIdx.x * kLaneBytes, static_cast<uint64_t>(col0) + kTileBytes <= g.len};
 }
 
 // rows 0..P-1 of tile t into the ring (clamped to k-1 when k < P)
@@ -325,9 +325,9 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ENC_MIN_WAVES : ECW_ENC_MIN_W
   // workgroup b takes tiles begin + b, + grid, + 2 grid, ... (concurrently
   // resident workgroups then cover adjacent columns of the same rows; giving
   // each workgroup a contiguous run of tiles measured 6-10 % slower)
-  uint64_t tile = g.tile_begin + blockIdx.x;
-  const uint64_t tend = g.tile_end;
-  const uint64_t tstep = gridDim.x;
+  uint32_t tile = g.tile_begin + blockIdx.x;
+  const uint32_t tend = g.tile_end;
+  const uint32_t tstep = gridDim.x;
   uint4 ring[P];
   // the first tile's row loads are issued before the table staging so the
   // two overlap
@@ -355,7 +355,7 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ENC_MIN_WAVES : ECW_ENC_MIN_W
       continue;
     }
     if (!have) ring_prologue<P, false>(ring, rows, g, cur);
-    const uint64_t nt = tile + tstep;
+    const uint32_t nt = tile + tstep;
     const TileAt nxt = tile_at(g, nt < tend ? nt : tile);
     const bool pf = cross && nt < tend && nxt.full;
     encode_tile<NW, P, LOCAL, false>(rows, g, cur, ring, pf, nxt, lds_base);
@@ -389,13 +389,29 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 #define ECW_ASM_MIN_WAVES_NW2 4  // 128 VGPRs: the 8-row tile uses 110
 #endif
 
+// Copy the packed tables (n16 x 16 B) into LDS, four loads in flight per lane
+// (one at a time, each waited for before its LDS write, took four round trips
+// at k = 128).
+__device__ __forceinline__ void stage_tables(uint8_t* lds, const uint4* __restrict__ tbl, int n16) {
+  uint4* l4 = reinterpret_cast<uint4*>(lds);
+  int i = threadIdx.x;
+  for (; i + 3 * kBlock < n16; i += 4 * kBlock) {
+    const uint4 a = tbl[i], b = tbl[i + kBlock], c = tbl[i + 2 * kBlock], d = tbl[i + 3 * kBlock];
+    l4[i] = a;
+    l4[i + kBlock] = b;
+    l4[i + 2 * kBlock] = c;
+    l4[i + 3 * kBlock] = d;
+  }
+  for (; i < n16; i += kBlock) l4[i] = tbl[i];
+}
+
 // Next tile of a ticket-ordered launch (EncodeGeom::ticket): lane 0 of the
 // workgroup takes a ticket, the slot after the LDS tables hands it to the rest.
-__device__ __forceinline__ uint64_t take_ticket(const EncodeGeom& g, unsigned long long* slot) {
+__device__ __forceinline__ uint32_t take_ticket(const EncodeGeom& g, uint32_t* slot) {
   __syncthreads();  // every wave has read the previous ticket
-  if (threadIdx.x == 0) *slot = g.tile_begin + (atomicAdd(g.ticket, 1ull) - g.ticket_base);
+  if (threadIdx.x == 0) *slot = g.tile_begin + static_cast<uint32_t>(atomicAdd(g.ticket, 1ull));
   __syncthreads();
-  return *slot;
+  return __builtin_amdgcn_readfirstlane(*slot);
 }
 
 template <int LOCAL, bool PARK, class Rows, int NW = 1>
@@ -404,54 +420,71 @@ __global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_W
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int n16 = g.k * 8 * NW;
 #ifndef ECW_DIAG_NOSTAGE  // diagnostic builds only: time the encode without staging its tables
-  for (int i = threadIdx.x; i < n16; i += kBlock) reinterpret_cast<uint4*>(lds)[i] = tbl[i];
+  stage_tables(lds, tbl, n16);
   __syncthreads();
 #else
   (void)n16;
 #endif
-  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds)));
   const int k = __builtin_amdgcn_readfirstlane(g.k);
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
   const uint32_t wmask = __builtin_amdgcn_readfirstlane(g.wmask), ww = __builtin_amdgcn_readfirstlane(g.wwidth);
+  const uint32_t lane_col = threadIdx.x * kLaneBytes;
   // the ticket slot sits after the tables: a static __shared__ variable would
   // shift the table records off the 64*NW alignment the LDS addressing relies on
-  unsigned long long* slot = reinterpret_cast<unsigned long long*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
+  uint32_t* slot = reinterpret_cast<uint32_t*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
   const bool tickets = g.ticket != nullptr;
-  for (uint64_t tile = tickets ? take_ticket(g, slot) : g.tile_begin + wg_slot(); tile < g.tile_end;
-       tile = tickets ? take_ticket(g, slot) : tile + gridDim.x) {
-    const TileAt cur = tile_at(g, tile);
-    if (cur.full) {
-      if constexpr (std::is_same<Rows, SlabRows>::value) {
-        const uint64_t bs = rows.bstride, pbs = rows.pbstride;
-        const uint8_t* sb = uniform_ptr(rows.base + static_cast<uint64_t>(cur.s) * rows.sstride);
-        const uint8_t* pb = uniform_ptr(rows.pbase + static_cast<uint64_t>(cur.s) * rows.psstride);
-        encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * pbs),
-                                                const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * pbs), bs,
-                                                pbs, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col, wmask, ww);
-      } else if constexpr (std::is_same<Rows, PtrTabRows>::value) {
-        // this stripe's rows of the device pointer tables, read with s_load
-        const uint64_t s = static_cast<uint64_t>(cur.s);
-        const uint8_t* st = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.src + s * k));
-        const uint8_t* dt = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.dst + s * rows.np));
-        encode_tile_asm<LOCAL, PARK, true, NW>(st, const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.m) * sizeof(void*)),
-                                           const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.row0) * sizeof(void*)),
-                                           0, 0, k, r, nrows, __builtin_amdgcn_readfirstlane(lds_base), cur.col,
-                                           wmask, ww);
-      } else {
-        const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
-            reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
-        const uint8_t* dtab = ka + offsetof(PtrRows, dst);
-        encode_tile_asm<LOCAL, PARK, true, NW>(ka + offsetof(PtrRows, src),
-                                           const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
-                                           const_cast<uint8_t*>(dtab), 0, 0, k, r, nrows,
-                                           __builtin_amdgcn_readfirstlane(lds_base), cur.col, wmask, ww);
-      }
+  // Full column tiles only (tile = stripe * per.d + column tile; the ragged
+  // last tile of every block is encode_tail_kernel's): nothing but the asm
+  // tile and a few scalar instructions per tile, so nothing lives in scratch
+  // and no compiler-issued memory operation drains the ring between tiles.
+  for (uint32_t tile = tickets ? take_ticket(g, slot) : g.tile_begin + static_cast<uint32_t>(wg_slot());
+       tile < g.tile_end; tile = tickets ? take_ticket(g, slot) : tile + gridDim.x) {
+    const uint32_t s = fast_div(tile, g.per);
+    if (s >= static_cast<uint32_t>(g.stripes)) break;  // never past the batch, whatever the launch says
+    const uint32_t col = (tile - s * g.per.d) * kTileBytes + lane_col;
+    if constexpr (std::is_same<Rows, SlabRows>::value) {
+      const uint64_t bs = rows.bstride, pbs = rows.pbstride;
+      const uint8_t* sb = uniform_ptr(rows.base + static_cast<uint64_t>(s) * rows.sstride);
+      const uint8_t* pb = uniform_ptr(rows.pbase + static_cast<uint64_t>(s) * rows.psstride);
+      encode_tile_asm<LOCAL, PARK, false, NW>(sb, const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.m) * pbs),
+                                              const_cast<uint8_t*>(pb + static_cast<uint64_t>(g.row0) * pbs), bs,
+                                              pbs, k, r, nrows, lds_base, col, wmask, ww);
+    } else if constexpr (std::is_same<Rows, PtrTabRows>::value) {
+      // this stripe's rows of the device pointer tables, read with s_load
+      const uint8_t* st = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.src + static_cast<uint64_t>(s) * k));
+      const uint8_t* dt = uniform_ptr(reinterpret_cast<const uint8_t*>(rows.dst + static_cast<uint64_t>(s) * rows.np));
+      encode_tile_asm<LOCAL, PARK, true, NW>(st, const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.m) * sizeof(void*)),
+                                             const_cast<uint8_t*>(dt + static_cast<uint64_t>(g.row0) * sizeof(void*)),
+                                             0, 0, k, r, nrows, lds_base, col, wmask, ww);
     } else {
-      uint4 ring[kPrefetchEncAsmTail];
-      ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
-      encode_tile<NW, kPrefetchEncAsmTail, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
+      const uint8_t* ka = uniform_ptr(reinterpret_cast<const uint8_t*>(
+          reinterpret_cast<uintptr_t>(__builtin_amdgcn_kernarg_segment_ptr())));
+      const uint8_t* dtab = ka + offsetof(PtrRows, dst);
+      encode_tile_asm<LOCAL, PARK, true, NW>(ka + offsetof(PtrRows, src),
+                                             const_cast<uint8_t*>(dtab + static_cast<uint64_t>(nrows) * sizeof(void*)),
+                                             const_cast<uint8_t*>(dtab), 0, 0, k, r, nrows, lds_base, col, wmask, ww);
     }
+  }
+}
+
+// The ragged last column tile of every stripe's blocks (len % kTileBytes != 0)
+// for the asm launches, one workgroup per stripe: byte-granular loads and
+// stores through the compiler-scheduled tile.
+template <int NW, int LOCAL, class Rows>
+__global__ __launch_bounds__(kBlock) void encode_tail_kernel(const Rows rows, const EncodeGeom g,
+                                                             const uint4* __restrict__ tbl) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  stage_tables(lds, tbl, g.k * 8 * NW);
+  __syncthreads();
+  const uint32_t lds_base = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(lds));
+  const uint32_t col0 = static_cast<uint32_t>(g.len / kTileBytes) * kTileBytes;
+  for (int s = blockIdx.x; s < g.stripes; s += gridDim.x) {
+    const TileAt cur{s, col0 + threadIdx.x * kLaneBytes, false};
+    uint4 ring[kPrefetchEncAsmTail];
+    ring_prologue<kPrefetchEncAsmTail, true>(ring, rows, g, cur);
+    encode_tile<NW, kPrefetchEncAsmTail, LOCAL, true>(rows, g, cur, ring, false, cur, lds_base);
   }
 }
 
@@ -513,11 +546,11 @@ __device__ __forceinline__ void xor_tile(const Args& a, const XorGeom& g, int s,
 }
 
 template <int P, class Args>
-__global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom g) {
-  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
-  for (uint64_t tile = wg_slot(); tile < total; tile += gridDim.x) {
-    const int s = static_cast<int>(tile / g.tiles);
-    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+__global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom g, const FastDiv per) {
+  const uint32_t total = static_cast<uint32_t>(g.stripes) * per.d;
+  for (uint32_t tile = static_cast<uint32_t>(wg_slot()); tile < total; tile += gridDim.x) {
+    const int s = static_cast<int>(fast_div(tile, per));
+    const uint32_t col0 = (tile - static_cast<uint32_t>(s) * per.d) * kTileBytes;
     const uint32_t col = col0 + threadIdx.x * kLaneBytes;
     if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
       xor_tile<P, false>(a, g, s, col);
@@ -569,11 +602,11 @@ __device__ __forceinline__ void xor_tile_fixed(const Args& a, const XorGeom& g, 
 }
 
 template <int N, class Args>
-__global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g) {
-  const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
-  for (uint64_t tile = wg_slot(); tile < total; tile += gridDim.x) {
-    const int s = static_cast<int>(tile / g.tiles);
-    const uint32_t col0 = static_cast<uint32_t>(tile - static_cast<uint64_t>(s) * g.tiles) * kTileBytes;
+__global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g, const FastDiv per) {
+  const uint32_t total = static_cast<uint32_t>(g.stripes) * per.d;
+  for (uint32_t tile = static_cast<uint32_t>(wg_slot()); tile < total; tile += gridDim.x) {
+    const int s = static_cast<int>(fast_div(tile, per));
+    const uint32_t col0 = (tile - static_cast<uint32_t>(s) * per.d) * kTileBytes;
     const uint32_t col = col0 + threadIdx.x * kLaneBytes;
     if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
       xor_tile_fixed<N, false>(a, g, s, col);
@@ -646,6 +679,65 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(uint8_t* dst, uint64_t bst
 constexpr int kPrefetchEnc = ECW_PREFETCH_ENC;
 constexpr int kPrefetchXor = ECW_PREFETCH_XOR;
 
+// Tile indices are 32-bit (FastDiv): one launch covers at most this many
+// tiles; larger batches go in several launches over consecutive stripes.
+constexpr uint64_t kMaxTilesPerLaunch = 1ull << 31;
+
+// The same rows from stripe s0 on (a batch split into several launches).
+inline PtrRows offset_stripes(const PtrRows& r, int, int) { return r; }  // one stripe
+inline SlabRows offset_stripes(const SlabRows& r, int s0, int) {
+  SlabRows o = r;
+  o.base += static_cast<uint64_t>(s0) * r.sstride;
+  o.pbase += static_cast<uint64_t>(s0) * r.psstride;
+  return o;
+}
+inline PtrTabRows offset_stripes(const PtrTabRows& r, int s0, int k) {
+  PtrTabRows o = r;
+  o.src += static_cast<uint64_t>(s0) * k;
+  o.dst += static_cast<uint64_t>(s0) * r.np;
+  return o;
+}
+inline XorPtr offset_stripes(const XorPtr& a, int) { return a; }  // one stripe
+inline XorSlab offset_stripes(const XorSlab& a, int s0) {
+  XorSlab o = a;
+  o.base += static_cast<uint64_t>(s0) * a.sstride;
+  o.out += static_cast<uint64_t>(s0) * a.ostride;
+  return o;
+}
+inline XorSplit offset_stripes(const XorSplit& a, int s0) {
+  XorSplit o = a;
+  o.base += static_cast<uint64_t>(s0) * a.sstride;
+  o.pbase += static_cast<uint64_t>(s0) * a.psstride;
+  o.out += static_cast<uint64_t>(s0) * a.ostride;
+  return o;
+}
+inline XorTab offset_stripes(const XorTab& a, int s0) {
+  XorTab o = a;
+  o.src += static_cast<uint64_t>(s0) * a.n;
+  o.dst += s0;
+  return o;
+}
+
+// ECW_DEBUG_LAUNCH=1 (debugging aid): every launch is printed with its grid
+// and synchronised, so a faulting kernel names itself.
+bool debug_launch() {
+  static const bool on = [] {
+    const char* e = std::getenv("ECW_DEBUG_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+hipError_t launched(const char* what, dim3 grid, size_t lds, hipStream_t s) {
+  hipError_t e = hipGetLastError();
+  if (debug_launch()) {
+    std::fprintf(stderr, "ecw launch %s grid %u lds %zu: %s", what, grid.x, lds, hipGetErrorString(e));
+    const hipError_t f = hipStreamSynchronize(s);
+    std::fprintf(stderr, " -> %s\n", hipGetErrorString(f));
+    if (e == hipSuccess) e = f;
+  }
+  return e;
+}
+
 unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
   // memory-bound streaming: enough workgroups to fill 256 CUs many deep,
   // grid-stride beyond that (encode tables are staged once per workgroup)
@@ -666,7 +758,24 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
     default:
       hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
   }
-  return hipGetLastError();
+  return launched("encode_kernel", grid, lds, s);
+}
+
+template <class Rows, int NW>
+hipError_t launch_encode_tail(const Rows& rows, const EncodeGeom& g, const uint4* tbl, hipStream_t s) {
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
+  const dim3 grid(static_cast<unsigned>(g.stripes < 65536 ? g.stripes : 65536));
+  switch (g.local_mode) {
+    case kLocalXor:
+      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    case kLocalZero:
+      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalZero, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      break;
+    default:
+      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalNone, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+  }
+  return launched("encode_tail_kernel", grid, lds, s);
 }
 
 template <class Rows, int NW>
@@ -685,7 +794,7 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
     default:
       hipLaunchKernelGGL((encode_kernel_asm<kLocalNone, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
   }
-  return hipGetLastError();
+  return launched("encode_kernel_asm", grid, lds, s);
 }
 
 // The slab is encoded in launch windows of one grid's worth of tiles (256 CUs x
@@ -758,79 +867,124 @@ void set_write_window(const Rows& rows, EncodeGeom& g) {
   g.wwidth = on ? w : 0;
 }
 
+// One launch range: stripes [0, g0.stripes) of `rows`, fewer than
+// kMaxTilesPerLaunch tiles. The asm kernel covers the full column tiles (in
+// launch windows, or in one ticket-ordered launch), encode_tail_kernel the
+// ragged last tile of every block; k = 1 (or ECW_ENC_ASM=0) takes the
+// compiler-scheduled kernel, which handles both.
 template <class Rows>
-hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s, TicketCounter* tc) {
-  const uint64_t total = static_cast<uint64_t>(g0.stripes) * g0.tiles;
-  if (total == 0) return hipSuccess;
-  if (g0.nrows < 1 || g0.nrows > kMaxPassRows || g0.k < 1 || g0.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  (void)hipGetLastError();  // report this call's launch errors, not an earlier one
-  const uint4* tbl = static_cast<const uint4*>(d_tbl);
+hipError_t launch_encode_range(const Rows& rows, const EncodeGeom& g0, const uint4* tbl, hipStream_t s,
+                               unsigned long long* ticket) {
+  const bool asm_tile = ECW_ENC_ASM && g0.k >= 2;
+  const uint64_t full = g0.len / kTileBytes;
+  const uint64_t per = asm_tile ? full : g0.tiles;  // tiles per stripe in the launch's numbering
+  const uint64_t total = static_cast<uint64_t>(g0.stripes) * per;
+  // what the kernels' 32-bit tile numbering assumes (the grid never covers a
+  // tile past the slab)
+  if (g0.stripes < 0 || total >= kMaxTilesPerLaunch || per > 0xFFFFFFFFull) return hipErrorInvalidValue;
   EncodeGeom gw = g0;
   set_write_window(rows, gw);
+  gw.per = make_fastdiv(static_cast<uint32_t>(per ? per : 1));
+  gw.ticket = nullptr;
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
                        : ECW_COHORT_TILES == 0 ? 256ull * ECW_GRID_PER_CU
                                                : total;
-  if (tc && tc->ptr && encode_uses_ticket(total, g0.k)) {
-    // one ticket-ordered launch; the caller holds the counter for this stream
+  if (asm_tile && ticket && total > 0 && encode_uses_ticket(total, g0.k)) {
+    // one ticket-ordered launch; the caller zeroed the counter for it
     EncodeGeom g = gw;
     g.tile_begin = 0;
-    g.tile_end = total;
-    g.ticket = tc->ptr;
-    g.ticket_base = tc->next;
+    g.tile_end = static_cast<uint32_t>(total);
+    g.ticket = ticket;
     const dim3 grid(grid_for(total));
     const hipError_t e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
                                       : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
-    if (e == hipSuccess) tc->next += total + grid.x;  // every workgroup draws one ticket past the end
-    return e;
-  }
-  for (uint64_t t0 = 0; t0 < total; t0 += win) {
-    EncodeGeom g = gw;
-    g.ticket = nullptr;
-    g.tile_begin = t0;
-    g.tile_end = t0 + win < total ? t0 + win : total;
-    const dim3 grid(grid_for(g.tile_end - g.tile_begin));
-    hipError_t e;
-    if (ECW_ENC_ASM && g.k >= 2) {
-      e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
-                       : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+    if (e != hipSuccess) return e;
+  } else {
+    for (uint64_t t0 = 0; t0 < total; t0 += win) {
+      EncodeGeom g = gw;
+      g.tile_begin = static_cast<uint32_t>(t0);
+      g.tile_end = static_cast<uint32_t>(t0 + win < total ? t0 + win : total);
+      const dim3 grid(grid_for(g.tile_end - g.tile_begin));
+      hipError_t e;
+      if (asm_tile)
+        e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+                         : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+      else
+        e = g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
       if (e != hipSuccess) return e;
-      continue;
     }
-    e = g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
+  }
+  if (asm_tile && full < g0.tiles)
+    return g0.nrows <= 4 ? launch_encode_tail<Rows, 1>(rows, gw, tbl, s) : launch_encode_tail<Rows, 2>(rows, gw, tbl, s);
+  return hipSuccess;
+}
+
+template <class Rows>
+hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_tbl, hipStream_t s,
+                         unsigned long long* ticket) {
+  if (static_cast<uint64_t>(g0.stripes) * g0.tiles == 0) return hipSuccess;
+  if (g0.nrows < 1 || g0.nrows > kMaxPassRows || g0.k < 1 || g0.len > 0xFFFFFFF0ull ||
+      g0.tiles != (g0.len + kTileBytes - 1) / kTileBytes || g0.tiles > kMaxTilesPerLaunch)
+    return hipErrorInvalidValue;
+  (void)hipGetLastError();  // report this call's launch errors, not an earlier one
+  const uint4* tbl = static_cast<const uint4*>(d_tbl);
+  const int per_launch = stripes_per_launch(g0.tiles);
+  if (g0.stripes <= per_launch) return launch_encode_range(rows, g0, tbl, s, ticket);
+  for (int64_t s0 = 0; s0 < g0.stripes; s0 += per_launch) {  // (no ticket: the counter serves one launch)
+    EncodeGeom g = g0;
+    g.stripes = static_cast<int>(g0.stripes - s0 < per_launch ? g0.stripes - s0 : per_launch);
+    const hipError_t e = launch_encode_range(offset_stripes(rows, static_cast<int>(s0), g0.k), g, tbl, s, nullptr);
     if (e != hipSuccess) return e;
   }
   return hipSuccess;
 }
 
 template <int N, class Args>
-hipError_t launch_xor_fixed(const Args& a, const XorGeom& g, dim3 grid, hipStream_t s) {
+hipError_t launch_xor_fixed(const Args& a, const XorGeom& g, const FastDiv& per, dim3 grid, hipStream_t s) {
   if constexpr (N >= 1) {
-    if (g.n < N) return launch_xor_fixed<N - 1>(a, g, grid, s);
-    hipLaunchKernelGGL((xor_kernel_fixed<N, Args>), grid, dim3(kBlock), 0, s, a, g);
-    return hipGetLastError();
+    if (g.n < N) return launch_xor_fixed<N - 1>(a, g, per, grid, s);
+    hipLaunchKernelGGL((xor_kernel_fixed<N, Args>), grid, dim3(kBlock), 0, s, a, g, per);
+    return launched("xor_kernel_fixed", grid, 0, s);
   }
   return hipErrorInvalidValue;
 }
 
 template <class Args>
-hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
+hipError_t launch_xor_range(const Args& a, const XorGeom& g, hipStream_t s) {
   const uint64_t total = static_cast<uint64_t>(g.stripes) * g.tiles;
   if (total == 0) return hipSuccess;
-  if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull) return hipErrorInvalidValue;
-  (void)hipGetLastError();  // report this call's launch error, not an earlier one
+  if (g.stripes < 0 || total >= kMaxTilesPerLaunch) return hipErrorInvalidValue;  // 32-bit tile numbering
   // ring depth <= n: the ring refills past the last row re-read row n-1, so a
   // depth-8 ring over 1-2 sources would load every byte up to 8 times
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR)), block(kBlock);
-  if (g.n <= ECW_XOR_FIXED_MAX) return launch_xor_fixed<ECW_XOR_FIXED_MAX>(a, g, grid, s);
+  const FastDiv per = make_fastdiv(static_cast<uint32_t>(g.tiles));
+  if (g.n <= ECW_XOR_FIXED_MAX) return launch_xor_fixed<ECW_XOR_FIXED_MAX>(a, g, per, grid, s);
   if (g.n <= 1)
-    hipLaunchKernelGGL((xor_kernel<1, Args>), grid, block, 0, s, a, g);
+    hipLaunchKernelGGL((xor_kernel<1, Args>), grid, block, 0, s, a, g, per);
   else if (g.n <= 2)
-    hipLaunchKernelGGL((xor_kernel<2, Args>), grid, block, 0, s, a, g);
+    hipLaunchKernelGGL((xor_kernel<2, Args>), grid, block, 0, s, a, g, per);
   else if (g.n <= 4)
-    hipLaunchKernelGGL((xor_kernel<4, Args>), grid, block, 0, s, a, g);
+    hipLaunchKernelGGL((xor_kernel<4, Args>), grid, block, 0, s, a, g, per);
   else
-    hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), grid, block, 0, s, a, g);
-  return hipGetLastError();
+    hipLaunchKernelGGL((xor_kernel<kPrefetchXor, Args>), grid, block, 0, s, a, g, per);
+  return launched("xor_kernel", grid, 0, s);
+}
+
+template <class Args>
+hipError_t launch_xor(const Args& a, const XorGeom& g, hipStream_t s) {
+  if (static_cast<uint64_t>(g.stripes) * g.tiles == 0) return hipSuccess;
+  if (g.n < 1 || g.n > kMaxSrc || g.len > 0xFFFFFFF0ull || g.tiles > kMaxTilesPerLaunch) return hipErrorInvalidValue;
+  (void)hipGetLastError();  // report this call's launch error, not an earlier one
+  // tile indices are 32-bit: batches of more than kMaxTilesPerLaunch tiles go
+  // in several launches over consecutive stripe ranges
+  const int per_launch = stripes_per_launch(g.tiles);
+  for (int64_t s0 = 0; s0 < g.stripes; s0 += per_launch) {
+    XorGeom gs = g;
+    gs.stripes = static_cast<int>(g.stripes - s0 < per_launch ? g.stripes - s0 : per_launch);
+    const hipError_t e = launch_xor_range(offset_stripes(a, static_cast<int>(s0)), gs, s);
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 // ---- small-stripe request service (ecw_internal.hpp SvcCtl) ----------------
@@ -853,9 +1007,10 @@ struct SvcReq {
   uint8_t* data;
   uint8_t* out;
   unsigned long long len, cs;
+  unsigned long long serial;
   int k, nrows, m, r, groups, local_mode, nw, flags;
 };
-constexpr int kSvcReqWords = 9;
+constexpr int kSvcReqWords = 10;
 static_assert(sizeof(SvcReq) == 8 * kSvcReqWords, "SvcReq mirrors the request words of SvcSlot");
 static_assert(offsetof(SvcSlot, flags) + sizeof(int) - offsetof(SvcSlot, tbl) == sizeof(SvcReq), "SvcSlot request layout");
 
@@ -1032,7 +1187,7 @@ __device__ __forceinline__ void svc_request(const SvcReq& q, uint32_t lds_base, 
 // exited_epoch. A request posted as part 0 leaves waits for the next epoch
 // (the host relaunches on exited_epoch), which serves it whole. A request's
 // tables stay staged in LDS while the next request uses the same codec (same
-// table address).
+// codec serial: a destroyed codec's successor may get the same table address).
 constexpr unsigned long long kSvcLeave = ~0ull;  // SvcDev::Slot::seq: part 0 has left
 #ifndef ECW_SVC_COLD_SLEEPS
 #define ECW_SVC_COLD_SLEEPS 2  // s_sleep 127 (~3.4 us each) after every poll of a cold slot
@@ -1053,8 +1208,9 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
   unsigned long long last = sys_load(&slot->done[part]);
   unsigned long long served = t0;      // wall clock of this part's latest request (polling speed)
   unsigned long long req_gen = ~0ull;  // generation of the request words held in LDS (none yet)
-  const uint4* staged = nullptr;       // tables in LDS
+  unsigned long long staged = 0;       // serial of the codec whose tables are in LDS (serials start at 1)
   int staged_n16 = 0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) sys_store(&ctl->started_epoch, epoch);
 #if ECW_SVC_TRACE
   unsigned long long trace[5] = {0, 0, 0, 0, 0};  // tools only: detect, words, start, computed, fenced
 #endif
@@ -1131,9 +1287,9 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
     }
     const SvcReq& q = *req;  // read from LDS (a private copy would live in scratch)
     const int n16 = q.k * 8 * q.nw;
-    if (q.tbl != staged || n16 != staged_n16) {
+    if (q.serial != staged || n16 != staged_n16) {
       for (int i = threadIdx.x; i < n16; i += kSvcThreads) reinterpret_cast<uint4*>(lds)[i] = q.tbl[i];
-      staged = q.tbl;
+      staged = q.serial;
       staged_n16 = n16;
       __syncthreads();
     }
@@ -1179,16 +1335,16 @@ hipError_t launch_service(SvcCtl* d_ctl, SvcDev* d_state, unsigned long long epo
 }
 
 hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
-                             TicketCounter* tc) {
-  return launch_encode(rows, g, d_tbl, s, tc);
+                             unsigned long long* ticket) {
+  return launch_encode(rows, g, d_tbl, s, ticket);
 }
 hipError_t launch_encode_slab(const SlabRows& slab, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
-                              TicketCounter* tc) {
-  return launch_encode(slab, g, d_tbl, s, tc);
+                              unsigned long long* ticket) {
+  return launch_encode(slab, g, d_tbl, s, ticket);
 }
 hipError_t launch_encode_tab(const PtrTabRows& rows, const EncodeGeom& g, const void* d_tbl, hipStream_t s,
-                             TicketCounter* tc) {
-  return launch_encode(rows, g, d_tbl, s, tc);
+                             unsigned long long* ticket) {
+  return launch_encode(rows, g, d_tbl, s, ticket);
 }
 bool encode_uses_ticket(uint64_t tiles, int k) {
   return ECW_ENC_ASM && k >= 2 && ECW_TICKET_MIN_TILES > 0 && tiles >= ECW_TICKET_MIN_TILES;
@@ -1211,7 +1367,12 @@ hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, 
   (void)hipGetLastError();  // report this launch's error, not an earlier one
   hipLaunchKernelGGL(fill_kernel, grid, dim3(kBlock), 0, s, dst, bstride, sstride, stripes, nblocks, len,
                      piece, pstride, offset, seed, s0, b0);
-  return hipGetLastError();
+  return launched("fill_kernel", grid, 0, s);
+}
+
+int stripes_per_launch(uint64_t tiles) {
+  const uint64_t n = kMaxTilesPerLaunch / (tiles ? tiles : 1);
+  return n > 0x7FFFFFFFull ? 0x7FFFFFFF : static_cast<int>(n);
 }
 
 int device_cu_count(int device) {

@@ -42,14 +42,14 @@ namespace {
 using Key = std::tuple<char, int, int, int, int, int, int, long long>;
 
 // codecs are immutable after creation: one per parameter set for the life of
-// the library, released when it is unloaded
-struct Codecs : std::map<Key, ecw_codec*> {
-  ~Codecs() {
-    for (auto& kv : *this) ecw_codec_destroy(kv.second);
-  }
-};
+// the process. The cache is never destroyed: at JVM exit other Java threads
+// may still be inside a native call on one of its codecs (System.exit does not
+// wait for them), so releasing the codecs from a static destructor could free
+// them under those calls. The map stays reachable through g_codecs, so leak
+// checkers do not report it.
+using Codecs = std::map<Key, ecw_codec*>;
 std::mutex g_mu;
-Codecs g_codecs;
+Codecs& g_codecs = *new Codecs();
 std::atomic<bool> g_xori_called{false};
 
 void throw_java(JNIEnv* e, const char* cls, const std::string& msg) {

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "ecwide.h"
+#include "../../ecwide_amd/csrc/ecw_internal.hpp"  // FastDiv (the kernels' tile -> stripe division)
 
 extern "C" {
 // libecw_isal.so (ecw_isal_shim.cpp), isal:include/erasure_code.h signatures
@@ -243,7 +244,43 @@ static void jni() {
   CHECK(jd_live_refs() == 0);
 }
 
+// ecw::fast_div == n / d for divisors 1..2^16, powers of two, large and
+// extreme divisors, against edge and pseudo-random numerators
+static void fastdiv() {
+  std::vector<uint32_t> ds;
+  for (uint32_t d = 1; d <= 65536; ++d) ds.push_back(d);
+  for (int b = 17; b < 32; ++b) {
+    ds.push_back(1u << b);
+    ds.push_back((1u << b) - 1);
+    ds.push_back((1u << b) + 1);
+  }
+  for (uint32_t d : {0x7FFFFFFFu, 0x80000000u, 0x80000001u, 0xFFFFFFFEu, 0xFFFFFFFFu, 3000000019u, 1234567891u}) ds.push_back(d);
+  uint64_t x = 0x9E3779B97F4A7C15ull;
+  int bad = 0;
+  for (uint32_t d : ds) {
+    const ecw::FastDiv f = ecw::make_fastdiv(d);
+    const uint32_t edge[] = {0u, 1u, d - 1, d, d + 1, 2 * d - 1, 2 * d, 0x7FFFFFFFu, 0x80000000u, 0xFFFFFFFEu, 0xFFFFFFFFu};
+    for (uint32_t n : edge)
+      if (ecw::fast_div(n, f) != n / d) ++bad;
+    for (int i = 0; i < 64; ++i) {
+      x ^= x << 13, x ^= x >> 7, x ^= x << 17;
+      const uint32_t n = static_cast<uint32_t>(x >> (i & 31));
+      if (ecw::fast_div(n, f) != n / d) ++bad;
+    }
+  }
+  CHECK(bad == 0);
+  // launch ranges of the 32-bit tile numbering
+  CHECK(ecw::stripes_per_launch(1) == 0x7FFFFFFF);
+  CHECK(ecw::stripes_per_launch(2) == (1 << 30));
+  CHECK(ecw::stripes_per_launch(16384) == (1 << 17));
+  CHECK(ecw::stripes_per_launch(1ull << 31) == 1);
+  for (uint64_t t : {1ull, 2ull, 3ull, 4097ull, 1ull << 20})
+    CHECK(static_cast<uint64_t>(ecw::stripes_per_launch(t)) * t < (1ull << 31) + t &&
+          static_cast<uint64_t>(ecw::stripes_per_launch(t)) * t <= (1ull << 31));
+}
+
 int main() {
+  fastdiv();
   schemes();
   codecs();
   isal_shim();

@@ -851,21 +851,26 @@ def test_errors_are_loud(E, torch):
 def test_chunk_generator_replay(E, orc, tmp_path):
     """BASELINE config #1 plumbing: ChunkGenerator with the default-style
     scheme (CL k=32, r=11, m=3; small chunk) writes D/G/L files whose bytes
-    equal the oracle's encode of the same source blocks."""
+    equal the reference's: the oracle's encode of the same source blocks with
+    ECWide-C's all-zero L blocks by default (NativeCodec.cc:181-186, as the JNI
+    drop-in), the XOR locals with --xor."""
     import os
 
     from ecwide_amd.chunk_generator import main
 
     (tmp_path / "scheme.ini").write_text("codeType = CL\nk = 32\ngroupDataNum = 11\nglobalParityNum = 3\n"
                                          "chunkSizeBits = 16\n")
-    (tmp_path / "settings.ini").write_text(f"chunksDir = {tmp_path / 'chunks'}\nmultiNodeEncode = true\n")
-    assert main(["urandom", "toy", "--scheme", str(tmp_path / "scheme.ini"),
-                 "--settings", str(tmp_path / "settings.ini")]) == 0
-    d = tmp_path / "chunks"
-    files = sorted(os.listdir(d))
-    assert len(files) == 38
-    data = [np.fromfile(d / f"{j + 1 + j // 11}_D_{j}", np.uint8) for j in range(32)]
-    want = orc.codec("C", 32, 3, 11, 1 << 16).encode(data)
     names = [f"{36 + i}_G_{i}" for i in range(3)] + ["12_L_0", "24_L_1", "35_L_2"]
-    for n, w in zip(names, want):
-        assert np.array_equal(np.fromfile(d / n, np.uint8), w), n
+    for extra, literal in (([], True), (["--xor"], False)):
+        out = tmp_path / ("chunks_xor" if extra else "chunks")
+        (tmp_path / "settings.ini").write_text(f"chunksDir = {out}\nmultiNodeEncode = true\n")
+        assert main(["urandom", "toy", "--scheme", str(tmp_path / "scheme.ini"),
+                     "--settings", str(tmp_path / "settings.ini"), *extra]) == 0
+        files = sorted(os.listdir(out))
+        assert len(files) == 38
+        data = [np.fromfile(out / f"{j + 1 + j // 11}_D_{j}", np.uint8) for j in range(32)]
+        want = orc.codec("C", 32, 3, 11, 1 << 16).encode(data, literal=literal)
+        for n, w in zip(names, want):
+            assert np.array_equal(np.fromfile(out / n, np.uint8), w), n
+        if literal:
+            assert all(not np.fromfile(out / n, np.uint8).any() for n in names[3:])  # zero L files

@@ -161,26 +161,47 @@ def _bench(*args, env=None):
     return p, (json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None)
 
 
-def test_bench_gpus2_launches_two_ranks_configs4_default():
+def test_bench_gpus2_launches_two_ranks_weak_default_and_configs4_leg():
     """`bench.py --gpus 2` (no torch.distributed.run around it) starts 2 ranks
-    itself; the N>1 default is configs[4]: the 256-stripe HBM-filling batch
-    (B sized so the whole batch fits one GPU, same B on every rank) split by
-    stripe; the reported time is the max over ranks."""
+    itself. Its main leg is the N=1 workload on EVERY rank (8 stripes of 64 MiB
+    per GPU, weak scaling; distinct stripe ids per rank); the configs[4] leg
+    splits the 256-stripe HBM-filling batch (B sized so the whole batch fits
+    one GPU, the same B on every rank) by stripe; the reported time is the
+    max over ranks."""
     p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-free-gib", "287")
     assert p.returncode == 0, p.stderr[-2000:]
-    assert line["n_gpus"] == 2 and line["scaling"] == "strong" and line["hbm_fill"]
-    assert line["stripes_total"] == 256 and line["block_bytes"] == 8 << 20
-    sh = line["shares"]
-    assert [(x["s0"], x["stripes"]) for x in sh] == [(0, 128), (128, 128)]
-    assert {x["block_bytes"] for x in sh} == {8 << 20}
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak" and not line["hbm_fill"]
+    assert line["stripes_total"] == 16 and line["block_bytes"] == 64 << 20
+    assert [(x["s0"], x["stripes"]) for x in line["shares"]] == [(0, 8), (8, 8)]
+    c4 = line["configs4"]
+    assert c4["stripes_total"] == 256 and c4["block_bytes"] == 8 << 20
+    assert [(x["s0"], x["stripes"]) for x in c4["shares"]] == [(0, 128), (128, 128)]
     assert line["el_max"] == max(line["rank_seconds"]) and len(line["rank_seconds"]) == 2
 
 
-def test_bench_dry_run_weak_and_column_modes():
-    p, line = _bench("--gpus", "2", "--dry-run", "--weak")
+def test_bench_config_same_at_every_n():
+    """SCALE's N=1 point is BENCH: the N=1 and N>1 lines carry the same
+    `config` apart from stripes_total (n_gpus is top-level)."""
+    lines = {}
+    for n in (1, 2, 4):
+        p, line = _bench("--gpus", str(n), "--dry-run")
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines[n] = line
+    base = dict(lines[1]["config"])
+    assert base["stripes_total"] == 8 and base["stripes_per_gpu"] == 8 and base["k"] == 128
+    assert base["block_bytes"] == 64 << 20 and "per GPU" in base["workload"]
+    for n in (2, 4):
+        c = dict(lines[n]["config"])
+        assert c.pop("stripes_total") == 8 * n
+        assert c == {x: v for x, v in base.items() if x != "stripes_total"}
+        assert lines[n]["n_gpus"] == n and lines[n]["scaling"] == "weak"
+
+
+def test_bench_dry_run_strong_and_column_modes():
+    p, line = _bench("--gpus", "2", "--dry-run", "--strong", "--stripes", "6")
     assert p.returncode == 0, p.stderr[-2000:]
-    assert line["scaling"] == "weak" and line["stripes_total"] == 16
-    assert [(x["s0"], x["stripes"]) for x in line["shares"]] == [(0, 8), (8, 8)]
+    assert line["scaling"] == "strong" and line["stripes_total"] == 6
+    assert [(x["s0"], x["stripes"]) for x in line["shares"]] == [(0, 3), (3, 3)]
     # fewer stripes than ranks: byte columns of every stripe, aligned to the tiled piece
     p, line = _bench("--gpus", "3", "--dry-run", "--strong", "--stripes", "1")
     assert p.returncode == 0, p.stderr[-2000:]
@@ -189,6 +210,11 @@ def test_bench_dry_run_weak_and_column_modes():
     assert sum(x["block_bytes"] for x in sh) == 64 << 20
     for a, b in zip(sh, sh[1:]):
         assert a["col_offset"] + a["block_bytes"] == b["col_offset"]
+    # --hbm-fill: the configs[3] batch is the main leg, split by stripe
+    p, line = _bench("--gpus", "2", "--dry-run", "--hbm-fill")
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert line["hbm_fill"] and line["scaling"] == "strong" and line["stripes_total"] == 256
+    assert line["configs4"] is None
 
 
 def test_bench_rejects_world_size_mismatch():
