@@ -286,6 +286,58 @@ def test_ticket_launch_matches_windows(E, torch, orc, k, m, r, B, S, layout, loc
             assert torch.equal(p[-W:], first[n][i]), ("second encode", s, i)
 
 
+def test_ticket_launches_on_per_thread_streams(E, torch, orc):
+    """ticket-ordered launches from two threads on
+    hipStreamPerThread (one stream handle, two real streams) must not share a
+    ticket counter. Each thread encodes its own 1 GiB-per-row slab (one
+    ticket launch each) four times, concurrently with the other; every
+    result equals the oracle on column windows of the first and last stripe
+    (tiles skipped by a clobbered counter would leave their parities at the
+    0xEE the slabs were poisoned with)."""
+    import ctypes
+    import threading
+
+    k, m, r, B, S = 4, 2, 2, 256 << 20, 4
+    per_thread = ctypes.c_void_p(2)  # hipStreamPerThread
+    slabs = []
+    for t in range(2):
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+        slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+        assert slab.encode_launches() == 1  # one ticket-ordered launch
+        slab.fill_random(seed=600 + t)
+        slabs.append(slab)
+    torch.cuda.synchronize()
+    errs = []
+
+    def work(t):
+        try:
+            for _ in range(4):
+                for s in range(S):
+                    for p in slabs[t].parity(s):
+                        p.fill_(0xEE)
+                torch.cuda.synchronize()
+                slabs[t].encode(stream=per_thread)
+                torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+
+    th = [threading.Thread(target=work, args=(t,)) for t in range(2)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errs, errs
+    W = 8192
+    oc = orc.codec("C", k, m, r, W)
+    for t, slab in enumerate(slabs):
+        for s in (0, S - 1):
+            par = slab.parity(s)
+            for off in (0, B // 2, B - W):
+                want = oc.encode([orc.fill(W, 600 + t, s, j, off) for j in range(k)])
+                for i, w in enumerate(want):
+                    assert np.array_equal(par[i][off:off + W].cpu().numpy(), w), (t, s, off, i)
+
+
 @pytest.mark.parametrize("k,m,r,local,layout", [
     (128, 3, 27, "xor", "blocks"),    # parked locals (the bench shape's tile); auto = on
     (32, 6, 8, "xor", "blocks"),      # 5-8 rows: the u64-entry (NW=2) tile

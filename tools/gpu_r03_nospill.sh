@@ -1,9 +1,7 @@
 # Round 3: the spill-free encode (r03.so) against round 2's build (base.so):
-# GPU suite first, then interleaved A/B on one allocation per layout, then the
-# WRITE_SIZE pass of the new tiled encode.
+# interleaved A/B on one allocation per layout, the FETCH/WRITE_SIZE passes of
+# the new tiled encode, then the default bench line.
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r03_pytest_gpu.log 2>&1 || { tail -40 gpurun_out/r03_pytest_gpu.log; exit 1; }
-tail -3 gpurun_out/r03_pytest_gpu.log
 O=gpurun_out/r03_nospill_ab.log
 B=build/variants/base.so; N=build/variants/r03.so
 echo "== tiled (8 KiB pieces, parities apart)" > $O
@@ -21,3 +19,5 @@ timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $GRAFT_REP
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $GRAFT_REPO_ROOT/gpurun_out/r03_enc_f_new -o run -- $P > $GRAFT_REPO_ROOT/gpurun_out/r03_enc_f_new.log 2>&1 || exit $?
 cd $GRAFT_REPO_ROOT
 python tools/pmc_kernels.py gpurun_out/r03_enc_w_new gpurun_out/r03_enc_f_new | tee gpurun_out/r03_encode_pmc_new.log
+timeout -k 10 600 python bench.py > gpurun_out/r03_bench_first.log 2>&1 || { tail -30 gpurun_out/r03_bench_first.log; exit 1; }
+grep -v amdgpu.ids gpurun_out/r03_bench_first.log | tail -3
