@@ -57,6 +57,11 @@
   "v_perm_b32 " A7 ", v32, v35, s53\n\t"
 
 // lo-nibble products at +0, hi-nibble products at +64 of the record
+#if defined(ECW_ASM_ABLATE) && ECW_ASM_ABLATE == 2
+// tuning builds only: every VALU instruction of the math, no LDS lookup (the
+// folds take the addresses)
+#define ECW_DW_READ(A0, A1, A2, A3, A4, A5, A6, A7)
+#else
 #define ECW_DW_READ(A0, A1, A2, A3, A4, A5, A6, A7) \
   "ds_read_b32 " A0 ", " A0 "\n\t"                   \
   "ds_read_b32 " A1 ", " A1 " offset:64\n\t"         \
@@ -66,6 +71,7 @@
   "ds_read_b32 " A5 ", " A5 " offset:64\n\t"         \
   "ds_read_b32 " A6 ", " A6 "\n\t"                   \
   "ds_read_b32 " A7 ", " A7 " offset:64\n\t"
+#endif
 
 #define ECW_DW_FOLD(C0, C1, C2, C3, A0, A1, A2, A3, A4, A5, A6, A7) \
   "v_bitop3_b32 " C0 ", " C0 ", " A0 ", " A1 " bitop3:0x96\n\t"      \
@@ -82,7 +88,7 @@
 
 // One data row from ring slot R0..R3 (s46 = its LDS table record): GF
 // products into the accumulators, XOR into the local parity (XL = 1).
-#ifndef ECW_ASM_ABLATE
+#if !defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2
 #define ECW_ROW(R0, R1, R2, R3, XL)                                   \
   "s_lshr_b32 s47, s46, 8\n\t"                                        \
   "s_and_b32 s48, s46, 0xff\n\t"                                      \

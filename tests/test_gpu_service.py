@@ -238,3 +238,34 @@ def test_codec_lifetime_beside_busy_service(E, orc):
           f"ms max, bulk encode {np.median(rates):.1f} GB/s (median) with {sum(calls)} service calls")
     assert max(destroy_s) < 0.05, destroy_s
     assert max(grow_s) < 0.05 + transfer, grow_s
+
+
+def test_service_restages_tables_of_a_recreated_codec(E, orc):
+    """the service keeps a codec's tables staged in LDS while the
+    next request uses the same codec. A codec destroyed and recreated with the
+    same shape but another matrix can get the same device table address, so
+    the cache is keyed by a per-codec serial: every recreated codec's parities
+    must follow its own matrix."""
+    import ctypes
+
+    from ecwide_amd import _lib
+
+    L = _lib.load()
+    k, rows, ln = 11, 3, 4096
+    rng = np.random.default_rng(5)
+    data = [orc.fill(ln, 77, 0, j) for j in range(k)]
+    dp = (ctypes.c_void_p * k)(*[x.ctypes.data for x in data])
+    for it in range(12):
+        mat = rng.integers(1, 256, k * rows, dtype=np.uint8)
+        h = ctypes.c_void_p()
+        assert L.ecw_matrix_codec_create(mat.ctypes.data_as(_lib._u8p), k, rows, 0, ctypes.byref(h)) == 0
+        try:
+            par = [np.zeros(ln, np.uint8) for _ in range(rows)]
+            pp = (ctypes.c_void_p * rows)(*[x.ctypes.data for x in par])
+            for _ in range(3):  # the service keeps this codec's tables between calls
+                assert L.ecw_encode(h, dp, pp, ln) == 0
+            want = orc.encode_data(orc.init_tables(k, rows, mat), data, rows)
+            for i, w in enumerate(want):
+                assert np.array_equal(par[i], w), (it, i)
+        finally:
+            L.ecw_codec_destroy(h)
