@@ -56,6 +56,23 @@ int status_of(hipError_t e) { return e == hipSuccess ? ECW_OK : ECW_EDEVICE; }
 
 namespace svc {
 bool busy(int device);  // the request service's resident kernel is (or may be) running on `device`
+// Launch-path work is about to be queued on `device`: ask a running resident
+// kernel to leave, so the work is not queued behind it on a shared hardware
+// queue. hold: keep it from relaunching until release_hold (the caller waits
+// for its own work in between).
+void yield(int device, bool hold);
+void release_hold(int device);
+// RAII form for the blocking host-memory entry points
+struct Hold {
+  int device;
+  bool on;
+  explicit Hold(int d, bool take = true) : device(d), on(take) {
+    if (on) yield(d, true);
+  }
+  ~Hold() {
+    if (on) release_hold(device);
+  }
+};
 }  // namespace svc
 
 // ---- deferred release of device resources -----------------------------------
@@ -309,6 +326,7 @@ bool as_slab(const uint8_t* const* src, int k, uint8_t* const* dst, int np, Slab
 
 int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) {
   const int k = c->k(), m = c->m(), ng = c->groups();
+  svc::yield(c->device, false);  // not queued behind the request service's resident kernel
   EncodeTarget t = t0;
   SlabRows strided;
   if (!t.slab && t.stripes == 1 && as_slab(t.src, k, t.dst, c->info.parity_num, &strided)) t.slab = &strided;
@@ -400,6 +418,8 @@ int run_encode(ecw_codec* c, const EncodeTarget& t0, size_t len, hipStream_t s) 
 int run_xor_ptr(const uint8_t* const* src, int n, uint8_t* dst, size_t len, hipStream_t s) {
   if (n < 1 || n > kMaxSrc) return ECW_EINVAL;
   if (len == 0) return ECW_OK;
+  int dev = 0;
+  if (hipGetDevice(&dev) == hipSuccess) svc::yield(dev, false);
   XorPtr xp;
   std::memset(&xp, 0, sizeof xp);
   for (int i = 0; i < n; ++i) xp.src[i] = src[i];
@@ -732,6 +752,7 @@ int ecw_encode_ptrs_dev(ecw_codec* c, int stripes, const uint8_t* const* d_data_
   eg.m = m;
   const PtrTabRows rows{d_data_ptrs, d_parity_ptrs, c->info.parity_num};
   const int npass = (m + kMaxPassRows - 1) / kMaxPassRows;
+  svc::yield(c->device, false);
   for (int q = 0; q < npass; ++q) {
     eg.row0 = q * kMaxPassRows;
     eg.nrows = std::min(kMaxPassRows, m - eg.row0);
@@ -766,6 +787,7 @@ int ecw_xor_reduce_ptrs_dev(int device, int stripes, int n, const uint8_t* const
   if (len == 0 || stripes == 0) return ECW_OK;
   DeviceGuard g(device);
   if (!g.ok) return ECW_EDEVICE;
+  svc::yield(device, false);
   const XorTab t{d_src_ptrs, d_dst_ptrs, n};
   const XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
   return status_of(launch_xor_tab(t, xg, static_cast<hipStream_t>(stream)));
@@ -889,6 +911,7 @@ static int repair_rows(ecw_codec* c, const SlabRows& rows, int stripes, int lost
   if (!g.ok) return ECW_EDEVICE;
   XorGeom xg{len, (len + kTileBytes - 1) / kTileBytes, stripes, n};
   if (len == 0 || stripes == 0) return ECW_OK;
+  svc::yield(c->device, false);
   const int k = c->k();
   const bool one_region = rows.pbase == rows.base + static_cast<uint64_t>(k) * rows.bstride &&
                           rows.pbstride == rows.bstride && rows.psstride == rows.sstride;
@@ -1027,6 +1050,7 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
+  svc::Hold hold(c->device);  // not queued behind the request service's resident kernel
   if (!c->pipe) {
     c->pipe = new (std::nothrow) HostPipe();
     if (!c->pipe) return ECW_ENOMEM;
@@ -1115,6 +1139,10 @@ struct Service {
   unsigned long long epoch = 0;  // last epoch launched (0: none yet)
   unsigned long long idle_ticks = 0, life_ticks = 0;
   std::vector<int> free_slots;
+  // blocking launch-path calls in flight on this device (svc::Hold): while
+  // any, the resident kernel is not relaunched and new small calls take the
+  // launch path, so that work never queues behind it
+  std::atomic<int> holds{0};
   uint8_t* stage[kSvcSlots] = {};
   uint8_t* d_stage[kSvcSlots] = {};
   size_t stage_bytes[kSvcSlots] = {};
@@ -1153,9 +1181,12 @@ struct Service {
     return ECW_OK;
   }
 
-  // launch the next epoch unless the current one is still serving (under mu)
+  // launch the next epoch unless the current one is still serving, or a
+  // launch-path call holds it off (under mu; ECW_OK either way)
   int ensure_running() {
     if (epoch != 0 && __atomic_load_n(&ctl->exited_epoch, __ATOMIC_ACQUIRE) != epoch) return ECW_OK;
+    if (holds.load(std::memory_order_acquire) > 0) return ECW_OK;  // relaunched once the hold ends
+    __atomic_store_n(&ctl->stop, 0ull, __ATOMIC_RELEASE);  // a yield asked the previous epoch to leave
     DeviceGuard g(device);
     if (!g.ok || hipMemsetAsync(d_state, 0, sizeof(SvcDev), stream) != hipSuccess) return ECW_EDEVICE;
     if (launch_service(d_ctl, d_state, epoch + 1, idle_ticks, life_ticks, stream) != hipSuccess) return ECW_EDEVICE;
@@ -1198,6 +1229,27 @@ struct Service {
 
 std::mutex g_mu;
 std::map<int, Service*> g_services;  // one per device, kept for the life of the process
+
+Service* find(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_services.find(device);
+  return it == g_services.end() ? nullptr : it->second;
+}
+
+// (declared at the top)
+extern "C++" void yield(int device, bool hold) {
+  Service* sv = find(device);
+  if (!sv) return;
+  if (hold) sv->holds.fetch_add(1, std::memory_order_acq_rel);
+  std::lock_guard<std::mutex> lk(sv->mu);
+  // every part watches the stop flag; the next epoch starts with it cleared
+  if (sv->ctl && sv->epoch != 0 && __atomic_load_n(&sv->ctl->exited_epoch, __ATOMIC_ACQUIRE) != sv->epoch)
+    __atomic_store_n(&sv->ctl->stop, 1ull, __ATOMIC_RELEASE);
+}
+extern "C++" void release_hold(int device) {
+  Service* sv = find(device);
+  if (sv) sv->holds.fetch_sub(1, std::memory_order_acq_rel);
+}
 
 // (declared at the top) the resident kernel has been launched and has not
 // published its exit yet
@@ -1263,6 +1315,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     if (c->ensure_device() != ECW_OK) return kNotServed;  // the launch path reports the error
   }
   Service* sv = service_for(c->device);
+  if (sv->holds.load(std::memory_order_acquire) > 0) return kNotServed;  // launch-path work in flight
   const size_t cs = (len + 255) & ~static_cast<size_t>(255);
   int slot;
   {
@@ -1547,6 +1600,10 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
+  // bulk work is not queued behind the request service's resident kernel; a
+  // single small stripe that the service did not take (it is held off, or
+  // stopping) does not hold it off in turn
+  svc::Hold hold(c->device, !(stripes == 1 && len <= kSvcMaxLen));
   if (!c->pipe) {
     c->pipe = new (std::nothrow) HostPipe();
     if (!c->pipe) return ECW_ENOMEM;

@@ -88,7 +88,41 @@
 
 // One data row from ring slot R0..R3 (s46 = its LDS table record): GF
 // products into the accumulators, XOR into the local parity (XL = 1).
-#if !defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2
+#ifndef ECW_ASM_PIPE
+#define ECW_ASM_PIPE 1
+#endif
+#if ECW_ASM_PIPE && (!defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2)
+// Software-pipelined across rows: the row's last lookup set (Y, from R3) is
+// left in flight and folded after the next row's first set has been issued,
+// so the LDS lookups never drain at a row boundary -- not behind the next
+// ring slot's vmcnt wait either (ECW_ROW_DRAIN folds it after the last row;
+// the Y set is zero at the start of a tile, so the first fold is a no-op).
+#define ECW_ROW(R0, R1, R2, R3, XL)                                   \
+  "s_lshr_b32 s47, s46, 8\n\t"                                        \
+  "s_and_b32 s48, s46, 0xff\n\t"                                      \
+  "s_mul_i32 s48, s48, 0x01010101\n\t"                                \
+  "v_mov_b32 v32, s47\n\t"                                            \
+  ECW_ADDR_X(R0) ECW_READ_X                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_Y("v24", "v25", "v26", "v27")                              \
+  ECW_ADDR_Y(R1) ECW_READ_Y                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_X("v12", "v13", "v14", "v15")                              \
+  ECW_ADDR_X(R2) ECW_READ_X                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_Y("v16", "v17", "v18", "v19")                              \
+  ECW_ADDR_Y(R3) ECW_READ_Y                                           \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_X("v20", "v21", "v22", "v23")                              \
+  ECW_LACC_##XL(R0, R1, R2, R3)                                       \
+  "s_add_u32 s46, s46, 128\n\t"
+#define ECW_ROW_DRAIN "s_waitcnt lgkmcnt(0)\n\t" ECW_FOLD_Y("v24", "v25", "v26", "v27")
+#define ECW_ROW_YZERO                                                 \
+  "v_mov_b32 v49, 0\n\tv_mov_b32 v50, 0\n\tv_mov_b32 v51, 0\n\tv_mov_b32 v52, 0\n\t" \
+  "v_mov_b32 v53, 0\n\tv_mov_b32 v54, 0\n\tv_mov_b32 v55, 0\n\tv_mov_b32 v56, 0\n\t"
+#elif !defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2
+#define ECW_ROW_DRAIN
+#define ECW_ROW_YZERO
 #define ECW_ROW(R0, R1, R2, R3, XL)                                   \
   "s_lshr_b32 s47, s46, 8\n\t"                                        \
   "s_and_b32 s48, s46, 0xff\n\t"                                      \
@@ -109,6 +143,8 @@
   ECW_FOLD_Y("v24", "v25", "v26", "v27")                              \
   "s_add_u32 s46, s46, 128\n\t"
 #else  // tuning builds only: the memory stream without the GF math
+#define ECW_ROW_DRAIN
+#define ECW_ROW_YZERO
 #define ECW_ROW(R0, R1, R2, R3, XL) ECW_LACC_##XL(R0, R1, R2, R3) "s_add_u32 s46, s46, 128\n\t"
 #endif
 
@@ -210,6 +246,11 @@
 #define ECW_ROWPTR_INIT_SLAB "s_mov_b64 s[40:41], %[row0]\n\t"
 #define ECW_ROWPTR_INIT_TAB "s_load_dwordx2 s[40:41], %[row0], 0x0\n\ts_mov_b32 s60, 8\n\ts_waitcnt lgkmcnt(0)\n\t"
 #define ECW_NEXTROW_SLAB "s_add_u32 s40, s40, %[bslo]\n\ts_addc_u32 s41, s41, %[bshi]\n\t"
+// before a ring load: the row pointer it uses has arrived. TAB: the s_load
+// issued behind the previous ring load (the pipelined rows keep LDS lookups in
+// flight, so no lgkmcnt wait inside a row implies it); SLAB: pointers are sums.
+#define ECW_LDWAIT_SLAB
+#define ECW_LDWAIT_TAB "s_waitcnt lgkmcnt(0)\n\t"
 #define ECW_NEXTROW_TAB "s_load_dwordx2 s[40:41], %[row0], s60\n\ts_add_u32 s60, s60, 8\n\t"
 #define ECW_LPTR_INIT_SLAB "s_mov_b64 s[42:43], %[lrow0]\n\t"
 #define ECW_LPTR_INIT_TAB "s_mov_b32 s61, 0\n\t"
@@ -296,6 +337,7 @@
   "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
   "v_mov_b32 v24, 0\n\tv_mov_b32 v25, 0\n\tv_mov_b32 v26, 0\n\tv_mov_b32 v27, 0\n\t" \
   "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  ECW_ROW_YZERO                                                             \
   "s_mov_b32 s44, 0\n\t"                                                    \
   "s_mov_b32 s59, 0\n\t"                                                    \
   "s_mov_b32 s46, %[lds]\n\t"                                               \
@@ -307,10 +349,10 @@
   "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
   "s_cbranch_scc1 11f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW_##MODE                           \
+  ECW_ROW_A(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_A ECW_NEXTROW_##MODE                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW_##MODE                           \
+  ECW_ROW_B(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_B ECW_NEXTROW_##MODE                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_branch 10b\n\t"                                                        \
   /* 2 or 3 rows left (k - j); slot A holds row j, slot B row j+1 */        \
@@ -319,7 +361,7 @@
   "s_cmp_eq_u32 s49, 3\n\t"                                                 \
   "s_cbranch_scc0 12f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND ECW_LOAD_A                                              \
+  ECW_ROW_A(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_A                              \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
   ECW_ROW_B(XL) BND                                                         \
@@ -334,6 +376,7 @@
   "s_waitcnt vmcnt(0)\n\t"                                                  \
   ECW_ROW_B(XL) BND                                                         \
   "13:\n\t"                                                                 \
+  ECW_ROW_DRAIN                                                             \
   ECW_WRITE_WINDOW                                                          \
   END                                                                       \
   /* global rows: byte l of the packed accumulators -> output row l */      \
