@@ -91,13 +91,19 @@
 #ifndef ECW_ASM_PIPE
 #define ECW_ASM_PIPE 1
 #endif
+#ifndef ECW_ASM_EARLY_LOAD
+#define ECW_ASM_EARLY_LOAD 1
+#endif
 #if ECW_ASM_PIPE && (!defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2)
 // Software-pipelined across rows: the row's last lookup set (Y, from R3) is
 // left in flight and folded after the next row's first set has been issued,
 // so the LDS lookups never drain at a row boundary -- not behind the next
 // ring slot's vmcnt wait either (ECW_ROW_DRAIN folds it after the last row;
 // the Y set is zero at the start of a tile, so the first fold is a no-op).
-#define ECW_ROW(R0, R1, R2, R3, XL)                                   \
+// A row is split where its ring slot's registers are last read (ECW_ROW_PRE:
+// every address computed and the local XOR done; ECW_ROW_POST: the last
+// folds), so in slab mode the slot's next load is issued between the two.
+#define ECW_ROW_PRE(R0, R1, R2, R3, XL)                               \
   "s_lshr_b32 s47, s46, 8\n\t"                                        \
   "s_and_b32 s48, s46, 0xff\n\t"                                      \
   "s_mul_i32 s48, s48, 0x01010101\n\t"                                \
@@ -112,10 +118,11 @@
   "s_waitcnt lgkmcnt(8)\n\t"                                          \
   ECW_FOLD_Y("v16", "v17", "v18", "v19")                              \
   ECW_ADDR_Y(R3) ECW_READ_Y                                           \
-  "s_waitcnt lgkmcnt(8)\n\t"                                          \
-  ECW_FOLD_X("v20", "v21", "v22", "v23")                              \
   ECW_LACC_##XL(R0, R1, R2, R3)                                       \
   "s_add_u32 s46, s46, 128\n\t"
+#define ECW_ROW_POST                                                  \
+  "s_waitcnt lgkmcnt(8)\n\t"                                          \
+  ECW_FOLD_X("v20", "v21", "v22", "v23")
 #define ECW_ROW_DRAIN "s_waitcnt lgkmcnt(0)\n\t" ECW_FOLD_Y("v24", "v25", "v26", "v27")
 #define ECW_ROW_YZERO                                                 \
   "v_mov_b32 v49, 0\n\tv_mov_b32 v50, 0\n\tv_mov_b32 v51, 0\n\tv_mov_b32 v52, 0\n\t" \
@@ -123,7 +130,8 @@
 #elif !defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2
 #define ECW_ROW_DRAIN
 #define ECW_ROW_YZERO
-#define ECW_ROW(R0, R1, R2, R3, XL)                                   \
+#define ECW_ROW_POST
+#define ECW_ROW_PRE(R0, R1, R2, R3, XL)                               \
   "s_lshr_b32 s47, s46, 8\n\t"                                        \
   "s_and_b32 s48, s46, 0xff\n\t"                                      \
   "s_mul_i32 s48, s48, 0x01010101\n\t"                                \
@@ -145,8 +153,10 @@
 #else  // tuning builds only: the memory stream without the GF math
 #define ECW_ROW_DRAIN
 #define ECW_ROW_YZERO
-#define ECW_ROW(R0, R1, R2, R3, XL) ECW_LACC_##XL(R0, R1, R2, R3) "s_add_u32 s46, s46, 128\n\t"
+#define ECW_ROW_POST
+#define ECW_ROW_PRE(R0, R1, R2, R3, XL) ECW_LACC_##XL(R0, R1, R2, R3) "s_add_u32 s46, s46, 128\n\t"
 #endif
+#define ECW_ROW(R0, R1, R2, R3, XL) ECW_ROW_PRE(R0, R1, R2, R3, XL) ECW_ROW_POST
 
 #define ECW_LACC_0(R0, R1, R2, R3)
 #define ECW_LACC_1(R0, R1, R2, R3)     \
@@ -318,6 +328,18 @@
 #define ECW_LOAD_B "global_load_dwordx4 v[8:11], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_ROW_A(XL) ECW_ROW("v4", "v5", "v6", "v7", XL)
 #define ECW_ROW_B(XL) ECW_ROW("v8", "v9", "v10", "v11", XL)
+#define ECW_ROW_PRE_A(XL) ECW_ROW_PRE("v4", "v5", "v6", "v7", XL)
+#define ECW_ROW_PRE_B(XL) ECW_ROW_PRE("v8", "v9", "v10", "v11", XL)
+// A row whose ring slot is reloaded with the row two ahead. SLAB: the load
+// goes out as soon as the slot is consumed (between PRE and POST); TAB: after
+// the row, behind the wait for its row-pointer s_load (ECW_LDWAIT_TAB, which
+// drains the LDS lookups too).
+#if ECW_ASM_EARLY_LOAD
+#define ECW_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW_ROW_POST BND
+#else
+#define ECW_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW_ROW_POST BND LOAD NEXT
+#endif
+#define ECW_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
 
 // The whole tile. BND is the boundary code (ECW_BOUNDARY(ZL, MODE) or
 // nothing), XL whether rows are XOR-ed into the local parity, END the code
@@ -349,10 +371,10 @@
   "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
   "s_cbranch_scc1 11f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_A ECW_NEXTROW_##MODE                           \
+  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_B(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_B ECW_NEXTROW_##MODE                           \
+  ECW_STEP_##MODE(ECW_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND)                           \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_branch 10b\n\t"                                                        \
   /* 2 or 3 rows left (k - j); slot A holds row j, slot B row j+1 */        \
@@ -361,7 +383,7 @@
   "s_cmp_eq_u32 s49, 3\n\t"                                                 \
   "s_cbranch_scc0 12f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND ECW_LDWAIT_##MODE ECW_LOAD_A                              \
+  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                    \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
   ECW_ROW_B(XL) BND                                                         \

@@ -735,6 +735,50 @@ def test_random_sweep_vs_oracle(E, torch, orc):
             assert np.array_equal(pbuf[np_ - 1 - i].cpu().numpy(), wants[0][i]), ("ptr", trial, k, m, r, B, i)
 
 
+@pytest.mark.parametrize("code,k,m,r,B,S", [
+    ("R", 128, 12, 0, 3 * 4096 + 80, 2),   # RS(128, 12): one pass of the 16-row tile (was two passes)
+    ("R", 20, 9, 0, 4096, 3),              # 9 rows
+    ("C", 64, 16, 10, 8192 + 16, 2),       # 16 global rows + 7 XOR locals
+    ("C", 200, 10, 40, 4096 + 1, 1),       # wide k: 100 KiB of tables (> 64 KiB of dynamic LDS)
+    ("R", 128, 20, 0, 4096, 1),            # 20 rows: a 16-row pass and a 4-row pass
+])
+def test_more_than_8_global_rows(E, torch, orc, code, k, m, r, B, S):
+    """ECWide-C's RS / TL / CL codecs take any m (NativeCodec.java:20-54):
+    9-16 global rows run in ONE pass over the data (16-byte packed table
+    entries, ds_read_b128), more in passes of 16; slab mode, pointer mode
+    (blocks in reverse order) and device pointer tables, vs the oracle."""
+    if code == "R":
+        c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(k, m, B))
+    else:
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    oc = orc.codec(code, k, m, r if r else k, B)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B)
+    slab.fill_random(seed=77)
+    slab.encode()
+    torch.cuda.synchronize()
+    wants = [oc.encode([orc.fill(B, 77, s, j) for j in range(k)], threads=8) for s in range(S)]
+    for s in range(S):
+        for i, p in enumerate(slab.parity(s)):
+            assert np.array_equal(p.cpu().numpy(), wants[s][i]), ("slab", s, i)
+    np_ = c.parityNum
+    Bp = (B + 15) // 16 * 16  # rows 16-byte aligned
+    dbuf = torch.empty((k, Bp), dtype=torch.uint8, device="cuda")
+    pbuf = torch.full((np_, Bp), 0x5A, dtype=torch.uint8, device="cuda")
+    for j in range(k):
+        dbuf[k - 1 - j, :B].copy_(slab.block(0, j))
+    c.encodeData([dbuf[k - 1 - j, :B] for j in range(k)], [pbuf[np_ - 1 - i, :B] for i in range(np_)])
+    torch.cuda.synchronize()
+    for i in range(np_):
+        assert np.array_equal(pbuf[np_ - 1 - i, :B].cpu().numpy(), wants[0][i]), ("ptr", i)
+    data = [[slab.block(s, j).clone() for j in range(k)] for s in range(S)]
+    par = [[torch.full((B,), 0xA5, dtype=torch.uint8, device="cuda") for _ in range(np_)] for _ in range(S)]
+    c.encodeStripes(data, par)
+    torch.cuda.synchronize()
+    for s in range(S):
+        for i in range(np_):
+            assert np.array_equal(par[s][i].cpu().numpy(), wants[s][i]), ("tables", s, i)
+
+
 @pytest.mark.parametrize("B", [(20 << 20) + 37, (8 << 20), 4096 * 3 + 5])
 def test_host_pipeline_multi_chunk_and_repair(E, torch, orc, B):
     """ecw_encode / ecw_repair on host buffers larger than one 8 MiB pipeline
