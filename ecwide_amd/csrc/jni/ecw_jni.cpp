@@ -102,8 +102,11 @@ bool read_fields(JNIEnv* e, jobject o, Fields* f) {
 
 // k of the stripe. The Java object keeps k only as encodeDataNum, except for
 // CL multi-node encode where encodeDataNum is the node's group size
-// (NativeCodec.java:84-91): node 1 holds the last group, so k follows; other
-// nodes need it from the environment (ECWIDE_K).
+// (NativeCodec.java:84-91): node 1 holds the last group, so k follows. Other
+// nodes take k from the scheme file the Java side itself was built from --
+// every ECWide-C process reads "config/scheme.ini" relative to its working
+// directory (DataNode.java:48, MasterNode.java:64) -- or from ECWIDE_K, and
+// the file's scheme must agree with the object's fields.
 bool stripe_k(JNIEnv* e, const Fields& f, int* k) {
   if (f.code_type != 'C' || !f.multinode) {
     *k = f.encode_data_num;
@@ -113,13 +116,34 @@ bool stripe_k(JNIEnv* e, const Fields& f, int* k) {
     *k = (f.group_num - 1) * f.group_data_num + f.encode_data_num;
     return true;
   }
-  const char* env = std::getenv("ECWIDE_K");
-  if (!env || std::atoi(env) < 1) {
+  auto fits = [&](int kk) {  // CodingScheme.java:24-40: groupNum = ceil(k / groupDataNum)
+    return kk >= 1 && f.group_data_num >= 1 && (kk + f.group_data_num - 1) / f.group_data_num == f.group_num;
+  };
+  if (const char* env = std::getenv("ECWIDE_K")) {
+    if (!fits(std::atoi(env))) {
+      throw_java(e, "java/lang/IllegalStateException",
+                 std::string("ecwide: ECWIDE_K=") + env + " disagrees with groupNum/groupDataNum");
+      return false;
+    }
+    *k = std::atoi(env);
+    return true;
+  }
+  const char* path = std::getenv("ECWIDE_SCHEME");
+  if (!path) path = "config/scheme.ini";
+  ecw_scheme s;
+  if (ecw_scheme_from_ini(path, &s) != ECW_OK) {
     throw_java(e, "java/lang/IllegalStateException",
-               "ecwide: multi-node CL encode on node > 1 needs k (set ECWIDE_K)");
+               std::string("ecwide: multi-node CL encode on node > 1 needs the stripe's k: ") + path +
+                   " not readable (run from the ECWide-C directory, or set ECWIDE_SCHEME / ECWIDE_K)");
     return false;
   }
-  *k = std::atoi(env);
+  if (s.code_type != 'C' || s.group_data_num != f.group_data_num || s.global_parity_num != f.global_num ||
+      s.chunk_size != static_cast<size_t>(f.chunk_size) || !fits(s.k)) {
+    throw_java(e, "java/lang/IllegalStateException",
+               std::string("ecwide: ") + path + " does not describe this NativeCodec's scheme");
+    return false;
+  }
+  *k = s.k;
   return true;
 }
 

@@ -186,11 +186,42 @@ def test_errors_raise_java_exceptions(jni, manifest):
     o = jni.dbl.jd_object(b"NativeCodec")
     jni.dbl.jd_set_prim(o, b"chunkSize", b"J", B)
     assert jni.call("generateEncodeMatrix", o).startswith("java/lang/NoSuchFieldError")
-    # CL multi-node on node > 1 needs k
+    # CL multi-node on node > 1 needs k: no ECWIDE_K and no scheme file where the
+    # process runs (the repository root has no config/scheme.ini)
     os.environ.pop("ECWIDE_K", None)
+    os.environ.pop("ECWIDE_SCHEME", None)
     mf = dict(f, node=2, edn=f["r"])
     mc = JavaCodec(jni, mf, B, multinode=True, init=False)
-    assert jni.call("generateEncodeMatrix", mc.o).startswith("java/lang/IllegalStateException")
+    assert "scheme.ini not readable" in jni.call("generateEncodeMatrix", mc.o)
+
+
+def test_multinode_k_from_scheme_file(jni, orc, tmp_path, monkeypatch):
+    """Nodes > 1 of a CL multi-node encode: the object holds only the group size
+    (NativeCodec.java:84-91), so the natives read k from config/scheme.ini in the
+    working directory, the file every ECWide-C process was built from
+    (DataNode.java:48). The file must describe the object's scheme; ECWIDE_K, when
+    set, must agree with groupNum."""
+    k, m, r, B = 20, 3, 6, 1 << 12
+    g = -(-k // r)
+    full = orc.cauchy1(k + m, k)[k:]
+    monkeypatch.delenv("ECWIDE_K", raising=False)
+    monkeypatch.delenv("ECWIDE_SCHEME", raising=False)
+    (tmp_path / "config").mkdir()
+    ini = tmp_path / "config" / "scheme.ini"
+    ini.write_text(f"codeType = CL\nk = {k}\ngroupDataNum = {r}\nglobalParityNum = {m}\nchunkSizeBits = 12\n")
+    monkeypatch.chdir(tmp_path)
+    for node in range(2, g + 1):
+        c0 = (g - node) * r
+        c = JavaCodec(jni, dict(oracle_fields(orc, k, m, r, B, node), edn=r), B, multinode=True)
+        assert np.array_equal(c.matrix.reshape(m, r), full[:, c0:c0 + r]), node
+    f2 = dict(oracle_fields(orc, k, m, r, B, 2), edn=r)
+    ini.write_text(f"codeType = CL\nk = {k}\ngroupDataNum = {r}\nglobalParityNum = {m + 1}\nchunkSizeBits = 12\n")
+    bad = JavaCodec(jni, f2, B, multinode=True, init=False)
+    assert "does not describe" in jni.call("generateEncodeMatrix", bad.o)
+    monkeypatch.setenv("ECWIDE_K", str(k + r))  # one group too many
+    assert "disagrees" in jni.call("generateEncodeMatrix", bad.o)
+    monkeypatch.setenv("ECWIDE_K", str(k - 1))  # same groupNum: accepted
+    assert jni.call("generateEncodeMatrix", bad.o) == ""
 
 
 @pytest.mark.gpu
