@@ -75,7 +75,7 @@ inline std::vector<uint8_t> isal_tables(int k, int rows, const uint8_t* a) {
 // 128 * NW bytes, so the kernel's LDS address for (j, nibble) is
 // j * 128 * NW + nibble * 4 * NW (+ 64 * NW for the high nibble).
 inline std::vector<uint8_t> packed_pass_tables(const uint8_t* matrix, int k, int row0, int rows) {
-  const int nw = rows <= 4 ? 1 : rows <= 8 ? 2 : 4;  // packed entry: 4, 8 or 16 bytes
+  const int nw = rows <= 4 ? 1 : 2;
   const size_t es = 4 * static_cast<size_t>(nw);
   std::vector<uint8_t> img(static_cast<size_t>(k) * 32 * es, 0);
   for (int j = 0; j < k; ++j) {

@@ -10,8 +10,7 @@
 namespace ecw {
 
 constexpr int kMaxSrc = 256;      // k + m <= 256 for a GF(2^8) Cauchy code
-constexpr int kMaxPassRows = 16;  // global rows per encode pass (u128 packed entries above 8)
-constexpr int kMaxAsmRows = 8;    // the asm tile's rows (u32 / u64 entries); 9-16 take the compiler-scheduled tile
+constexpr int kMaxPassRows = 8;   // global rows per encode pass (u64 packed entries)
 constexpr int kMaxPtrLocals = 120;  // local outputs per pointer-mode encode pass
 #ifndef ECW_BLOCK
 #define ECW_BLOCK 256
