@@ -507,7 +507,41 @@
   ECW2_FOLD1(C1, D1, "v62", "v63", "v64", "v65")           \
   ECW2_FOLD1(C2, D2, "v66", "v67", "v68", "v69")           \
   ECW2_FOLD1(C3, D3, "v70", "v71", "v72", "v73")
-#define ECW2_ROW(R0, R1, R2, R3, XL)                                                   \
+#ifndef ECW2_ASM_PIPE
+#define ECW2_ASM_PIPE 1
+#endif
+#if ECW2_ASM_PIPE && ECW_ASM_PIPE && (!defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2)
+// Pipelined across rows as ECW_ROW_PRE / ECW_ROW_POST above: the row's last
+// lookup set (Y, from R3) is folded after the next row's first set is issued.
+#define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
+  "s_lshr_b32 s47, s46, 8\n\t"                                                         \
+  "s_and_b32 s48, s46, 0xff\n\t"                                                       \
+  "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
+  "v_mov_b32 v32, s47\n\t"                                                             \
+  ECW2_ADDR_X(R0) ECW2_READ_X                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_Y("v24", "v25", "v26", "v27", "v86", "v87", "v88", "v89")                 \
+  ECW2_ADDR_Y(R1) ECW2_READ_Y                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_X("v12", "v13", "v14", "v15", "v74", "v75", "v76", "v77")                 \
+  ECW2_ADDR_X(R2) ECW2_READ_X                                                          \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_Y("v16", "v17", "v18", "v19", "v78", "v79", "v80", "v81")                 \
+  ECW2_ADDR_Y(R3) ECW2_READ_Y                                                          \
+  ECW_LACC_##XL(R0, R1, R2, R3)                                                        \
+  "s_add_u32 s46, s46, 256\n\t"
+#define ECW2_ROW_POST                                                                  \
+  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
+  ECW2_FOLD_X("v20", "v21", "v22", "v23", "v82", "v83", "v84", "v85")
+#define ECW2_ROW_DRAIN \
+  "s_waitcnt lgkmcnt(0)\n\t" ECW2_FOLD_Y("v24", "v25", "v26", "v27", "v86", "v87", "v88", "v89")
+#define ECW2_ROW_YZERO                                                                 \
+  "v_mov_b32 v58, 0\n\tv_mov_b32 v59, 0\n\tv_mov_b32 v60, 0\n\tv_mov_b32 v61, 0\n\t"     \
+  "v_mov_b32 v62, 0\n\tv_mov_b32 v63, 0\n\tv_mov_b32 v64, 0\n\tv_mov_b32 v65, 0\n\t"     \
+  "v_mov_b32 v66, 0\n\tv_mov_b32 v67, 0\n\tv_mov_b32 v68, 0\n\tv_mov_b32 v69, 0\n\t"     \
+  "v_mov_b32 v70, 0\n\tv_mov_b32 v71, 0\n\tv_mov_b32 v72, 0\n\tv_mov_b32 v73, 0\n\t"
+#else
+#define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
   "s_lshr_b32 s47, s46, 8\n\t"                                                         \
   "s_and_b32 s48, s46, 0xff\n\t"                                                       \
   "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
@@ -526,8 +560,22 @@
   "s_waitcnt lgkmcnt(0)\n\t"                                                           \
   ECW2_FOLD_Y("v24", "v25", "v26", "v27", "v86", "v87", "v88", "v89")                 \
   "s_add_u32 s46, s46, 256\n\t"
+#define ECW2_ROW_POST
+#define ECW2_ROW_DRAIN
+#define ECW2_ROW_YZERO
+#endif
+#define ECW2_ROW(R0, R1, R2, R3, XL) ECW2_ROW_PRE(R0, R1, R2, R3, XL) ECW2_ROW_POST
 #define ECW2_ROW_A(XL) ECW2_ROW("v4", "v5", "v6", "v7", XL)
 #define ECW2_ROW_B(XL) ECW2_ROW("v8", "v9", "v10", "v11", XL)
+#define ECW2_ROW_PRE_A(XL) ECW2_ROW_PRE("v4", "v5", "v6", "v7", XL)
+#define ECW2_ROW_PRE_B(XL) ECW2_ROW_PRE("v8", "v9", "v10", "v11", XL)
+// as ECW_STEP_* for the 8-row rows
+#if ECW_ASM_EARLY_LOAD
+#define ECW2_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW2_ROW_POST BND
+#else
+#define ECW2_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW2_ROW_POST BND LOAD NEXT
+#endif
+#define ECW2_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW2_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
 
 #define ECW2_BOUNDARY_PARK                                  \
   "s_add_u32 s49, s44, 1\n\t"                               \
@@ -585,6 +633,7 @@
   "v_mov_b32 v82, 0\n\tv_mov_b32 v83, 0\n\tv_mov_b32 v84, 0\n\tv_mov_b32 v85, 0\n\t" \
   "v_mov_b32 v86, 0\n\tv_mov_b32 v87, 0\n\tv_mov_b32 v88, 0\n\tv_mov_b32 v89, 0\n\t" \
   "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  ECW2_ROW_YZERO                                                            \
   "s_mov_b32 s44, 0\n\t"                                                    \
   "s_mov_b32 s59, 0\n\t"                                                    \
   "s_mov_b32 s46, %[lds]\n\t"                                               \
@@ -595,10 +644,10 @@
   "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
   "s_cbranch_scc1 11f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW2_ROW_A(XL) BND ECW_LOAD_A ECW_NEXTROW_##MODE                          \
+  ECW2_STEP_##MODE(ECW2_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND) \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW2_ROW_B(XL) BND ECW_LOAD_B ECW_NEXTROW_##MODE                          \
+  ECW2_STEP_##MODE(ECW2_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND) \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_branch 10b\n\t"                                                        \
   "11:\n\t"                                                                 \
@@ -606,7 +655,7 @@
   "s_cmp_eq_u32 s49, 3\n\t"                                                 \
   "s_cbranch_scc0 12f\n\t"                                                  \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW2_ROW_A(XL) BND ECW_LOAD_A                                             \
+  ECW2_STEP_##MODE(ECW2_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                   \
   "s_add_u32 s44, s44, 1\n\t"                                               \
   "s_waitcnt vmcnt(1)\n\t"                                                  \
   ECW2_ROW_B(XL) BND                                                        \
@@ -621,6 +670,7 @@
   "s_waitcnt vmcnt(0)\n\t"                                                  \
   ECW2_ROW_B(XL) BND                                                        \
   "13:\n\t"                                                                 \
+  ECW2_ROW_DRAIN                                                            \
   ECW_WRITE_WINDOW                                                          \
   END                                                                       \
   /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \

@@ -5,6 +5,8 @@ cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
 L=$GRAFT_REPO_ROOT/ecwide_amd/libecwide.so
 P1=SQ_WAVE_CYCLES,SQ_BUSY_CYCLES,SQ_WAIT_ANY,SQ_WAIT_INST_ANY,SQ_ACTIVE_INST_ANY,SQ_ACTIVE_INST_VALU,SQ_ACTIVE_INST_LDS,SQ_LDS_BANK_CONFLICT
 P2=SQ_LDS_IDX_ACTIVE,SQ_WAIT_INST_LDS,SQ_INSTS_VALU,SQ_INSTS_LDS,SQ_INSTS_SALU,SQ_WAVES,SQ_ACTIVE_INST_SCA,SQ_INSTS_SMEM,GRBM_GUI_ACTIVE,GRBM_COUNT
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -k "more_than_8 or random_sweep" -x -q --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r03_pytest_m8.log 2>&1 || { tail -30 gpurun_out/r03_pytest_m8.log; exit 1; }
+tail -1 gpurun_out/r03_pytest_m8.log
 O=gpurun_out/r03_sq.log
 : > $O
 for m in 3 5 8; do
