@@ -1307,7 +1307,7 @@ Service* service_for(int device) {
 int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
   const int k = c->k(), m = c->m(), np = c->info.parity_num;
   const int nw = m <= 4 ? 1 : 2;
-  if (!enabled() || m < 1 || m > kMaxPassRows || len == 0 || len > kSvcMaxLen ||
+  if (!enabled() || m < 1 || m > kMaxSvcRows || len == 0 || len > kSvcMaxLen ||
       static_cast<size_t>(k) * 128 * nw > kSvcLds)
     return kNotServed;
   {

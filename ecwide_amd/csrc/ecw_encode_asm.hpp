@@ -713,6 +713,307 @@
   ECW2_TILE_OPERANDS, "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",       \
     "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109"
 
+// ---------------------------------------------------------------------------
+// 9-16 global rows (NW = 4): one 16-byte table entry per nibble (rows 4e..4e+3
+// in dword e; records of 512 B, lo-nibble entries at +0, hi at +256, so a
+// record's low byte is that of the table base), looked up with ds_read_b128
+// (4 LDS cycles, conflict-free: a lookup's 16 entries cover the 64 banks), and
+// four banks of 16 packed accumulators. One pass over the data instead of two
+// passes of <= 8 rows. The tables reach past 64 KiB for k > 128, so the record
+// address enters the lookup address with two bytes (selectors 0x0C0504xx).
+// Lookups go in sets of four (two data bytes, lo and hi): set X v[42:57], set Y
+// v[58:73], each tuple's address in its first register; nibble words v34/v35
+// (nibble * 16: lo = (W << 4) & 0xF0.., hi = W & 0xF0..), v33 = 0xF0F0F0F0.
+// Accumulators: rows 0-3 v[12:27], 4-7 v[74:89], 8-11 v[90:105], 12-15
+// v[106:121] (byte column c of the lane's 16 in the c-th register of each
+// bank); parked local parities v[122:141]. Rows are software-pipelined: the
+// last Y set of a row is folded after the next row's first X set is issued.
+#define ECW4_NIB(W)                                  \
+  "v_lshlrev_b32 v34, 4, " W "\n\t"                  \
+  "v_and_or_b32 v34, v34, v33, s48\n\t"              \
+  "v_and_or_b32 v35, " W ", v33, s48\n\t"
+// lookup addresses of two data bytes (selectors SA, SB) of the nibble words
+#define ECW4_ADDR(SA, SB, A0, A1, A2, A3)            \
+  "v_perm_b32 " A0 ", v32, v34, " SA "\n\t"          \
+  "v_perm_b32 " A1 ", v32, v35, " SA "\n\t"          \
+  "v_perm_b32 " A2 ", v32, v34, " SB "\n\t"          \
+  "v_perm_b32 " A3 ", v32, v35, " SB "\n\t"
+#define ECW4_ADDR_X01 ECW4_ADDR("s50", "s51", "v42", "v46", "v50", "v54")
+#define ECW4_ADDR_Y23 ECW4_ADDR("s52", "s53", "v58", "v62", "v66", "v70")
+#define ECW4_READ_X                                  \
+  "ds_read_b128 v[42:45], v42\n\t"                   \
+  "ds_read_b128 v[46:49], v46 offset:256\n\t"        \
+  "ds_read_b128 v[50:53], v50\n\t"                   \
+  "ds_read_b128 v[54:57], v54 offset:256\n\t"
+#define ECW4_READ_Y                                  \
+  "ds_read_b128 v[58:61], v58\n\t"                   \
+  "ds_read_b128 v[62:65], v62 offset:256\n\t"        \
+  "ds_read_b128 v[66:69], v66\n\t"                   \
+  "ds_read_b128 v[70:73], v70 offset:256\n\t"
+// byte column p: lo entry (L0..L3) ^ hi entry (H0..H3) into the four banks
+#define ECW4_FOLD1(C, D, E, F, L0, L1, L2, L3, H0, H1, H2, H3)     \
+  "v_bitop3_b32 " C ", " C ", " L0 ", " H0 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " D ", " D ", " L1 ", " H1 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " E ", " E ", " L2 ", " H2 " bitop3:0x96\n\t"      \
+  "v_bitop3_b32 " F ", " F ", " L3 ", " H3 " bitop3:0x96\n\t"
+// byte columns p and p + 1 from set X / set Y (P = p, Q = p + 1 as numbers)
+#define ECW4_FOLD_X(P, Q)                                                                           \
+  ECW4_FOLD1("v" #P, "v" ECW4_D(P), "v" ECW4_E(P), "v" ECW4_F(P), "v42", "v43", "v44", "v45", "v46", \
+             "v47", "v48", "v49")                                                                   \
+  ECW4_FOLD1("v" #Q, "v" ECW4_D(Q), "v" ECW4_E(Q), "v" ECW4_F(Q), "v50", "v51", "v52", "v53", "v54", \
+             "v55", "v56", "v57")
+#define ECW4_FOLD_Y(P, Q)                                                                           \
+  ECW4_FOLD1("v" #P, "v" ECW4_D(P), "v" ECW4_E(P), "v" ECW4_F(P), "v58", "v59", "v60", "v61", "v62", \
+             "v63", "v64", "v65")                                                                   \
+  ECW4_FOLD1("v" #Q, "v" ECW4_D(Q), "v" ECW4_E(Q), "v" ECW4_F(Q), "v66", "v67", "v68", "v69", "v70", \
+             "v71", "v72", "v73")
+// bank registers of byte column c (bank C: v12 + c): D = v74 + c, E = v90 + c,
+// F = v106 + c, spelled out (P is the bank-C register number 12..27)
+#define ECW4_D(P) ECW4_D_##P
+#define ECW4_E(P) ECW4_E_##P
+#define ECW4_F(P) ECW4_F_##P
+#define ECW4_D_12 "74"
+#define ECW4_D_13 "75"
+#define ECW4_D_14 "76"
+#define ECW4_D_15 "77"
+#define ECW4_D_16 "78"
+#define ECW4_D_17 "79"
+#define ECW4_D_18 "80"
+#define ECW4_D_19 "81"
+#define ECW4_D_20 "82"
+#define ECW4_D_21 "83"
+#define ECW4_D_22 "84"
+#define ECW4_D_23 "85"
+#define ECW4_D_24 "86"
+#define ECW4_D_25 "87"
+#define ECW4_D_26 "88"
+#define ECW4_D_27 "89"
+#define ECW4_E_12 "90"
+#define ECW4_E_13 "91"
+#define ECW4_E_14 "92"
+#define ECW4_E_15 "93"
+#define ECW4_E_16 "94"
+#define ECW4_E_17 "95"
+#define ECW4_E_18 "96"
+#define ECW4_E_19 "97"
+#define ECW4_E_20 "98"
+#define ECW4_E_21 "99"
+#define ECW4_E_22 "100"
+#define ECW4_E_23 "101"
+#define ECW4_E_24 "102"
+#define ECW4_E_25 "103"
+#define ECW4_E_26 "104"
+#define ECW4_E_27 "105"
+#define ECW4_F_12 "106"
+#define ECW4_F_13 "107"
+#define ECW4_F_14 "108"
+#define ECW4_F_15 "109"
+#define ECW4_F_16 "110"
+#define ECW4_F_17 "111"
+#define ECW4_F_18 "112"
+#define ECW4_F_19 "113"
+#define ECW4_F_20 "114"
+#define ECW4_F_21 "115"
+#define ECW4_F_22 "116"
+#define ECW4_F_23 "117"
+#define ECW4_F_24 "118"
+#define ECW4_F_25 "119"
+#define ECW4_F_26 "120"
+#define ECW4_F_27 "121"
+// One data row from ring slot R0..R3 (s46 = its LDS table record). PRE ends
+// where the slot's registers are last read; the previous row's last Y set
+// (byte columns 14, 15) is folded after this row's first X set is issued.
+#define ECW4_ROW_PRE(R0, R1, R2, R3, XL)           \
+  "s_lshr_b32 s47, s46, 8\n\t"                     \
+  "s_and_b32 s48, s46, 0xff\n\t"                   \
+  "s_mul_i32 s48, s48, 0x01010101\n\t"             \
+  "v_mov_b32 v32, s47\n\t"                         \
+  ECW4_NIB(R0) ECW4_ADDR_X01 ECW4_READ_X           \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_Y(26, 27)                              \
+  ECW4_ADDR_Y23 ECW4_READ_Y                        \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_X(12, 13)                              \
+  ECW4_NIB(R1) ECW4_ADDR_X01 ECW4_READ_X           \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_Y(14, 15)                              \
+  ECW4_ADDR_Y23 ECW4_READ_Y                        \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_X(16, 17)                              \
+  ECW4_NIB(R2) ECW4_ADDR_X01 ECW4_READ_X           \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_Y(18, 19)                              \
+  ECW4_ADDR_Y23 ECW4_READ_Y                        \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_X(20, 21)                              \
+  ECW4_NIB(R3) ECW4_ADDR_X01 ECW4_READ_X           \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_Y(22, 23)                              \
+  ECW4_ADDR_Y23 ECW4_READ_Y                        \
+  ECW_LACC_##XL(R0, R1, R2, R3)                    \
+  "s_add_u32 s46, s46, 512\n\t"
+#define ECW4_ROW_POST                              \
+  "s_waitcnt lgkmcnt(4)\n\t"                       \
+  ECW4_FOLD_X(24, 25)
+#define ECW4_ROW_DRAIN "s_waitcnt lgkmcnt(0)\n\t" ECW4_FOLD_Y(26, 27)
+#define ECW4_ROW_YZERO                                                                   \
+  "v_mov_b32 v58, 0\n\tv_mov_b32 v59, 0\n\tv_mov_b32 v60, 0\n\tv_mov_b32 v61, 0\n\t"     \
+  "v_mov_b32 v62, 0\n\tv_mov_b32 v63, 0\n\tv_mov_b32 v64, 0\n\tv_mov_b32 v65, 0\n\t"     \
+  "v_mov_b32 v66, 0\n\tv_mov_b32 v67, 0\n\tv_mov_b32 v68, 0\n\tv_mov_b32 v69, 0\n\t"     \
+  "v_mov_b32 v70, 0\n\tv_mov_b32 v71, 0\n\tv_mov_b32 v72, 0\n\tv_mov_b32 v73, 0\n\t"
+#define ECW4_ROW(R0, R1, R2, R3, XL) ECW4_ROW_PRE(R0, R1, R2, R3, XL) ECW4_ROW_POST
+#define ECW4_ROW_A(XL) ECW4_ROW("v4", "v5", "v6", "v7", XL)
+#define ECW4_ROW_B(XL) ECW4_ROW("v8", "v9", "v10", "v11", XL)
+#define ECW4_ROW_PRE_A(XL) ECW4_ROW_PRE("v4", "v5", "v6", "v7", XL)
+#define ECW4_ROW_PRE_B(XL) ECW4_ROW_PRE("v8", "v9", "v10", "v11", XL)
+#if ECW_ASM_EARLY_LOAD
+#define ECW4_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW4_ROW_POST BND
+#else
+#define ECW4_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW4_ROW_POST BND LOAD NEXT
+#endif
+#define ECW4_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW4_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
+
+#define ECW4_BOUNDARY_PARK                                  \
+  "s_add_u32 s49, s44, 1\n\t"                               \
+  "s_cmp_eq_u32 s49, s45\n\t"                               \
+  "s_cbranch_scc0 20f\n\t"                                  \
+  ECW_PARK(0, "v122", "v123", "v124", "v125", 21)           \
+  ECW_PARK(1, "v126", "v127", "v128", "v129", 22)           \
+  ECW_PARK(2, "v130", "v131", "v132", "v133", 23)           \
+  ECW_PARK(3, "v134", "v135", "v136", "v137", 24)           \
+  ECW_PARK(4, "v138", "v139", "v140", "v141", 25)           \
+  "26:\n\t"                                                 \
+  "s_add_u32 s59, s59, 1\n\t"                               \
+  "s_add_u32 s45, s45, %[r]\n\t"                            \
+  "s_min_u32 s45, s45, %[k]\n\t"                            \
+  ECW_LRESET_1                                              \
+  "20:\n\t"
+#define ECW4_STORE_PARKED(MODE)                                             \
+  ECW_LPTR_INIT_##MODE                                                      \
+  ECW_UNPARK(0, "v[122:125]", MODE) ECW_UNPARK(1, "v[126:129]", MODE)       \
+  ECW_UNPARK(2, "v[130:133]", MODE) ECW_UNPARK(3, "v[134:137]", MODE)       \
+  ECW_UNPARK(4, "v[138:141]", MODE)                                         \
+  "27:\n\t"
+
+#define ECW4_TILE_ASM(BND, XL, END, MODE)                                          \
+  "v_mov_b32 v40, %[col]\n\t"                                               \
+  "v_mov_b32 v33, 0xf0f0f0f0\n\t"                                           \
+  "s_mov_b32 s50, 0x0c050400\n\t"                                           \
+  "s_mov_b32 s51, 0x0c050401\n\t"                                           \
+  "s_mov_b32 s52, 0x0c050402\n\t"                                           \
+  "s_mov_b32 s53, 0x0c050403\n\t"                                           \
+  ECW_ROWPTR_INIT_##MODE                                                    \
+  ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
+  ECW_LOAD_B ECW_NEXTROW_##MODE                                             \
+  "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
+  "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
+  "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
+  "v_mov_b32 v24, 0\n\tv_mov_b32 v25, 0\n\tv_mov_b32 v26, 0\n\tv_mov_b32 v27, 0\n\t" \
+  "v_mov_b32 v74, 0\n\tv_mov_b32 v75, 0\n\tv_mov_b32 v76, 0\n\tv_mov_b32 v77, 0\n\t" \
+  "v_mov_b32 v78, 0\n\tv_mov_b32 v79, 0\n\tv_mov_b32 v80, 0\n\tv_mov_b32 v81, 0\n\t" \
+  "v_mov_b32 v82, 0\n\tv_mov_b32 v83, 0\n\tv_mov_b32 v84, 0\n\tv_mov_b32 v85, 0\n\t" \
+  "v_mov_b32 v86, 0\n\tv_mov_b32 v87, 0\n\tv_mov_b32 v88, 0\n\tv_mov_b32 v89, 0\n\t" \
+  "v_mov_b32 v90, 0\n\tv_mov_b32 v91, 0\n\tv_mov_b32 v92, 0\n\tv_mov_b32 v93, 0\n\t" \
+  "v_mov_b32 v94, 0\n\tv_mov_b32 v95, 0\n\tv_mov_b32 v96, 0\n\tv_mov_b32 v97, 0\n\t" \
+  "v_mov_b32 v98, 0\n\tv_mov_b32 v99, 0\n\tv_mov_b32 v100, 0\n\tv_mov_b32 v101, 0\n\t" \
+  "v_mov_b32 v102, 0\n\tv_mov_b32 v103, 0\n\tv_mov_b32 v104, 0\n\tv_mov_b32 v105, 0\n\t" \
+  "v_mov_b32 v106, 0\n\tv_mov_b32 v107, 0\n\tv_mov_b32 v108, 0\n\tv_mov_b32 v109, 0\n\t" \
+  "v_mov_b32 v110, 0\n\tv_mov_b32 v111, 0\n\tv_mov_b32 v112, 0\n\tv_mov_b32 v113, 0\n\t" \
+  "v_mov_b32 v114, 0\n\tv_mov_b32 v115, 0\n\tv_mov_b32 v116, 0\n\tv_mov_b32 v117, 0\n\t" \
+  "v_mov_b32 v118, 0\n\tv_mov_b32 v119, 0\n\tv_mov_b32 v120, 0\n\tv_mov_b32 v121, 0\n\t" \
+  "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  ECW4_ROW_YZERO                                                            \
+  "s_mov_b32 s44, 0\n\t"                                                    \
+  "s_mov_b32 s59, 0\n\t"                                                    \
+  "s_mov_b32 s46, %[lds]\n\t"                                               \
+  ECW_LPTR_INIT_##MODE                                                      \
+  "s_min_u32 s45, %[r], %[k]\n\t"                                           \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 3\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND) \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND) \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc0 12f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_ROW_B(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW4_ROW_A(XL) BND                                                        \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_ROW_A(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW4_ROW_B(XL) BND                                                        \
+  "13:\n\t"                                                                 \
+  ECW4_ROW_DRAIN                                                            \
+  ECW_WRITE_WINDOW                                                          \
+  END                                                                       \
+  /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \
+  ECW_GPTR_INIT_##MODE                                                      \
+  "s_mov_b32 s56, 0\n\t"                                                    \
+  "30:\n\t"                                                                 \
+  "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
+  "s_cbranch_scc1 31f\n\t"                                                  \
+  "s_and_b32 s49, s56, 3\n\t"                                               \
+  "s_add_u32 s57, s49, 4\n\t"                                               \
+  "s_lshl_b32 s58, s57, 24\n\t"                                             \
+  "s_lshl_b32 s57, s57, 8\n\t"                                              \
+  "s_or_b32 s57, s57, s49\n\t"                                              \
+  "s_or_b32 s57, s57, 0x0c0c0000\n\t"                                       \
+  "s_lshl_b32 s49, s49, 16\n\t"                                             \
+  "s_or_b32 s58, s58, s49\n\t"                                              \
+  "s_or_b32 s58, s58, 0x0c0c\n\t"                                           \
+  "s_cmp_ge_u32 s56, 8\n\t"                                                 \
+  "s_cbranch_scc1 36f\n\t"                                                  \
+  "s_cmp_ge_u32 s56, 4\n\t"                                                 \
+  "s_cbranch_scc1 32f\n\t"                                                  \
+  ECW2_TRANSPOSE("v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19",    \
+                 "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27")    \
+  "s_branch 33f\n\t"                                                        \
+  "32:\n\t"                                                                 \
+  ECW2_TRANSPOSE("v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81",    \
+                 "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89")    \
+  "s_branch 33f\n\t"                                                        \
+  "36:\n\t"                                                                 \
+  "s_cmp_ge_u32 s56, 12\n\t"                                                \
+  "s_cbranch_scc1 37f\n\t"                                                  \
+  ECW2_TRANSPOSE("v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97",    \
+                 "v98", "v99", "v100", "v101", "v102", "v103", "v104", "v105") \
+  "s_branch 33f\n\t"                                                        \
+  "37:\n\t"                                                                 \
+  ECW2_TRANSPOSE("v106", "v107", "v108", "v109", "v110", "v111", "v112", "v113", \
+                 "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121") \
+  "33:\n\t"                                                                 \
+  ECW_GPTR_GET_##MODE                                                       \
+  ECW_ASM_GSTORE("v[36:39]", "s[54:55]")                                    \
+  "s_nop 1\n\t"                                                             \
+  ECW_GPTR_NEXT_##MODE                                                      \
+  "s_add_u32 s56, s56, 1\n\t"                                               \
+  "s_branch 30b\n\t"                                                        \
+  "31:"
+
+#define ECW4_TILE_OPERANDS                                                          \
+  ECW2_TILE_OPERANDS, "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",        \
+    "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", \
+    "v112", "v113", "v114", "v115", "v116", "v117", "v118", "v119", "v120", "v121"
+#define ECW4_TILE_OPERANDS_PARK                                                     \
+  ECW4_TILE_OPERANDS, "v122", "v123", "v124", "v125", "v126", "v127", "v128", "v129", "v130",     \
+    "v131", "v132", "v133", "v134", "v135", "v136", "v137", "v138", "v139", "v140", "v141"
+
 namespace ecw {
 namespace {
 
@@ -747,14 +1048,34 @@ namespace {
                      ECW2_TILE_OPERANDS);                                                \
   }
 
-// NW = 1: <= 4 global rows (u32 table entries); NW = 2: 5-8 rows (u64 entries)
+#define ECW4_TILE_CALL(MODE)                                                             \
+  if constexpr (LOCAL == kLocalNone) {                                                   \
+    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW4_TILE_OPERANDS);         \
+  } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
+    asm volatile(ECW4_TILE_ASM(ECW4_BOUNDARY_PARK, 1, ECW4_STORE_PARKED(MODE), MODE)     \
+                     ECW4_TILE_OPERANDS_PARK);                                           \
+  } else if constexpr (LOCAL == kLocalXor) {                                             \
+    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW4_TILE_OPERANDS);     \
+  } else {                                                                               \
+    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
+                     ECW4_TILE_OPERANDS);                                                \
+  }
+
+// NW = 1: <= 4 global rows (u32 table entries); NW = 2: 5-8 rows (u64
+// entries); NW = 4: 9-16 rows (16-byte entries)
 template <int LOCAL, bool PARK, bool TAB, int NW = 1>
 __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lrow0, uint8_t* grow0, uint64_t bstride,
                                                 uint64_t pbstride, int k, int r, int nrows, uint32_t lds,
                                                 uint32_t col, uint32_t wmask, uint32_t ww) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
   const uint32_t pbslo = static_cast<uint32_t>(pbstride), pbshi = static_cast<uint32_t>(pbstride >> 32);
-  if constexpr (NW == 2) {
+  if constexpr (NW == 4) {
+    if constexpr (TAB) {
+      ECW4_TILE_CALL(TAB)
+    } else {
+      ECW4_TILE_CALL(SLAB)
+    }
+  } else if constexpr (NW == 2) {
     if constexpr (TAB) {
       ECW2_TILE_CALL(TAB)
     } else {

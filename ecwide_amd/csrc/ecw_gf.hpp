@@ -68,14 +68,14 @@ inline std::vector<uint8_t> isal_tables(int k, int rows, const uint8_t* a) {
   return g;
 }
 
-// Device table image for one pass of up to 8 global rows:
-// per data row j a record of 32 entries, entry type u32 (rows <= 4, NW = 1)
-// or u64 (rows <= 8, NW = 2). Entry n < 16 packs c_l * n of every row l of
+// Device table image for one pass of up to 16 global rows:
+// per data row j a record of 32 entries, entry type u32 (rows <= 4, NW = 1),
+// u64 (rows <= 8, NW = 2) or 16 bytes (rows <= 16, NW = 4). Entry n < 16 packs c_l * n of every row l of
 // the pass in byte l; entry 16 + n packs c_l * (n << 4). Record stride is
 // 128 * NW bytes, so the kernel's LDS address for (j, nibble) is
 // j * 128 * NW + nibble * 4 * NW (+ 64 * NW for the high nibble).
 inline std::vector<uint8_t> packed_pass_tables(const uint8_t* matrix, int k, int row0, int rows) {
-  const int nw = rows <= 4 ? 1 : 2;
+  const int nw = rows <= 4 ? 1 : rows <= 8 ? 2 : 4;  // packed entry: 4, 8 or 16 bytes
   const size_t es = 4 * static_cast<size_t>(nw);
   std::vector<uint8_t> img(static_cast<size_t>(k) * 32 * es, 0);
   for (int j = 0; j < k; ++j) {

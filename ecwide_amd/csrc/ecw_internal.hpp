@@ -10,7 +10,8 @@
 namespace ecw {
 
 constexpr int kMaxSrc = 256;      // k + m <= 256 for a GF(2^8) Cauchy code
-constexpr int kMaxPassRows = 8;   // global rows per encode pass (u64 packed entries)
+constexpr int kMaxPassRows = 16;  // global rows per encode pass (16-byte packed entries above 8)
+constexpr int kMaxSvcRows = 8;    // global rows the resident request service encodes
 constexpr int kMaxPtrLocals = 120;  // local outputs per pointer-mode encode pass
 #ifndef ECW_BLOCK
 #define ECW_BLOCK 256

@@ -51,6 +51,8 @@ __device__ __forceinline__ uint4 xor4(uint4 a, uint4 b) {
 
 typedef __attribute__((address_space(3))) const uint32_t lds_u32;
 typedef __attribute__((address_space(3))) const unsigned long long lds_u64;
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) const u32x4_t lds_u128;
 
 // Columns are 32-bit offsets from a wave-uniform row pointer, so loads and
 // stores use the SGPR-base + VGPR-offset form (blocks are < 4 GiB; the host
@@ -169,9 +171,11 @@ __device__ __forceinline__ uint8_t* local_row(const SlabRows& r, const EncodeGeo
 
 // ---- GF(2^8) multiply-accumulate of one 16-byte row slice -----------------
 // acc[p] (NW=1) packs the running products of byte column p for up to 4
-// rows; NW=2: acc[2p], acc[2p+1] pack 8 rows. `rec` is the LDS byte address
-// of row j's table record (a multiple of 64*NW): its bits 8.. enter the
-// address through v_perm (jhi), its low byte through the nibble mask (jlo).
+// rows; NW=2: acc[2p], acc[2p+1] pack 8 rows; NW=4: acc[4p..4p+3] pack 16
+// rows (one 16-byte LDS entry per nibble, ds_read_b128). `rec` is the LDS
+// byte address of row j's table record (a multiple of 128*NW): its bits 8..
+// enter the address through v_perm (jhi), its low byte through the nibble
+// mask (jlo).
 template <int NW>
 __device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], uint32_t rec) {
   const uint32_t jhi = rec >> 8;
@@ -181,12 +185,17 @@ __device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], 
   for (int d = 0; d < 4; ++d) {
     const uint32_t w = w4[d];
     // (nibble * entry size) in every byte, record low byte OR-ed in
-    const uint32_t lo = NW == 1 ? (((w << 2) & 0x3C3C3C3Cu) | jlo) : (((w << 3) & 0x78787878u) | jlo);
-    const uint32_t hi = NW == 1 ? (((w >> 2) & 0x3C3C3C3Cu) | jlo) : (((w >> 1) & 0x78787878u) | jlo);
+    const uint32_t lo = NW == 1   ? (((w << 2) & 0x3C3C3C3Cu) | jlo)
+                        : NW == 2 ? (((w << 3) & 0x78787878u) | jlo)
+                                  : (((w << 4) & 0xF0F0F0F0u) | jlo);
+    const uint32_t hi = NW == 1   ? (((w >> 2) & 0x3C3C3C3Cu) | jlo)
+                        : NW == 2 ? (((w >> 1) & 0x78787878u) | jlo)
+                                  : ((w & 0xF0F0F0F0u) | jlo);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      // address = jhi << 8 | byte b of lo/hi  (selector: S1.byte b, S0.byte0, 0, 0)
-      const uint32_t sel = 0x0C0C0400u | static_cast<uint32_t>(b);
+      // address = jhi << 8 | byte b of lo/hi  (selector: S1.byte b, S0.byte0,
+      // and S0.byte1 for the 16-row tables, which reach past 64 KiB at k > 128)
+      const uint32_t sel = (NW == 4 ? 0x0C050400u : 0x0C0C0400u) | static_cast<uint32_t>(b);
       const uint32_t al = __builtin_amdgcn_perm(jhi, lo, sel);
       const uint32_t ah = __builtin_amdgcn_perm(jhi, hi, sel);
       const int p = 4 * d + b;
@@ -194,11 +203,16 @@ __device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], 
         const uint32_t tl = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(al));
         const uint32_t th = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(ah + 64));
         acc[p] = xor3(acc[p], tl, th);
-      } else {
+      } else if constexpr (NW == 2) {
         const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al));
         const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah + 128));
         acc[2 * p] = xor3(acc[2 * p], static_cast<uint32_t>(tl), static_cast<uint32_t>(th));
         acc[2 * p + 1] = xor3(acc[2 * p + 1], static_cast<uint32_t>(tl >> 32), static_cast<uint32_t>(th >> 32));
+      } else {
+        const u32x4_t tl = *reinterpret_cast<lds_u128*>(static_cast<uintptr_t>(al));
+        const u32x4_t th = *reinterpret_cast<lds_u128*>(static_cast<uintptr_t>(ah + 256));
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[4 * p + e] = xor3(acc[4 * p + e], tl[e], th[e]);
       }
     }
   }
@@ -309,7 +323,15 @@ __device__ __forceinline__ void encode_tile(const Rows& rows, const EncodeGeom& 
       ring[p] = ld16<TAIL>(src_row(rows, g, use_next ? nxt.s : cur.s, row), use_next ? nxt.col : col, len);
     }
   }
-  for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
+  if constexpr (NW == 4) {
+    // unrolled over the 16 rows (constant accumulator indices: a runtime index
+    // into 64 accumulators puts them in scratch)
+#pragma unroll
+    for (int l = 0; l < 4 * NW; ++l)
+      if (l < g.nrows) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
+  } else {
+    for (int l = 0; l < g.nrows; ++l) st16<TAIL>(glob_row(rows, g, cur.s, l), col, len, unpack_row<NW>(acc, l));
+  }
 }
 
 template <int NW, int P, int LOCAL, class Rows>
@@ -319,7 +341,10 @@ template <int NW, int P, int LOCAL, class Rows>
 #ifndef ECW_ENC_MIN_WAVES_NW2
 #define ECW_ENC_MIN_WAVES_NW2 4  // 5-8 rows: 128 VGPRs (at 80 the 32 accumulators spill inside the row loop)
 #endif
-__global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ENC_MIN_WAVES : ECW_ENC_MIN_WAVES_NW2) void encode_kernel(const Rows rows, const EncodeGeom g,
+#ifndef ECW_ENC_MIN_WAVES_NW4
+#define ECW_ENC_MIN_WAVES_NW4 2  // 9-16 rows: 256 VGPRs for the 64 packed accumulators
+#endif
+__global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ENC_MIN_WAVES : NW == 2 ? ECW_ENC_MIN_WAVES_NW2 : ECW_ENC_MIN_WAVES_NW4) void encode_kernel(const Rows rows, const EncodeGeom g,
                                                         const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   // workgroup b takes tiles begin + b, + grid, + 2 grid, ... (concurrently
@@ -388,6 +413,9 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 #ifndef ECW_ASM_MIN_WAVES_NW2
 #define ECW_ASM_MIN_WAVES_NW2 4  // 128 VGPRs: the 8-row tile uses 110
 #endif
+#ifndef ECW_ASM_MIN_WAVES_NW4
+#define ECW_ASM_MIN_WAVES_NW4 3  // 168 VGPRs: the 16-row tile uses 142
+#endif
 
 // Copy the packed tables (n16 x 16 B) into LDS, four loads in flight per lane
 // (one at a time, each waited for before its LDS write, took four round trips
@@ -415,7 +443,9 @@ __device__ __forceinline__ uint32_t take_ticket(const EncodeGeom& g, uint32_t* s
 }
 
 template <int LOCAL, bool PARK, class Rows, int NW = 1>
-__global__ __launch_bounds__(kBlock, NW == 1 ? ECW_ASM_MIN_WAVES : ECW_ASM_MIN_WAVES_NW2) void encode_kernel_asm(
+__global__ __launch_bounds__(kBlock, NW == 1   ? ECW_ASM_MIN_WAVES
+                                    : NW == 2 ? ECW_ASM_MIN_WAVES_NW2
+                                              : ECW_ASM_MIN_WAVES_NW4) void encode_kernel_asm(
     const Rows rows, const EncodeGeom g, const uint4* __restrict__ tbl) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int n16 = g.k * 8 * NW;
@@ -745,18 +775,28 @@ unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
   return static_cast<unsigned>(tiles_total < cap ? (tiles_total ? tiles_total : 1) : cap);
 }
 
+// Launch with `lds` bytes of dynamic LDS; above 64 KiB (9-16-row tables of
+// wide stripes: k * 512 B) the kernel's limit is raised first (160 KiB per CU).
+template <class K, class... A>
+void launch_lds(K kernel, dim3 grid, size_t lds, hipStream_t s, const A&... a) {
+  if (lds > 65536)
+    (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
+                              static_cast<int>(lds));
+  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), lds, s, a...);
+}
+
 template <int NW, class Rows>
 hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
   const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
   switch (g.local_mode) {
     case kLocalXor:
-      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>, grid, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalZero, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalZero, Rows>, grid, lds, s, rows, g, tbl);
       break;
     default:
-      hipLaunchKernelGGL((encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>, grid, lds, s, rows, g, tbl);
   }
   return launched("encode_kernel", grid, lds, s);
 }
@@ -767,13 +807,13 @@ hipError_t launch_encode_tail(const Rows& rows, const EncodeGeom& g, const uint4
   const dim3 grid(static_cast<unsigned>(g.stripes < 65536 ? g.stripes : 65536));
   switch (g.local_mode) {
     case kLocalXor:
-      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalXor, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalXor, Rows>, grid, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalZero, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalZero, Rows>, grid, lds, s, rows, g, tbl);
       break;
     default:
-      hipLaunchKernelGGL((encode_tail_kernel<NW, kLocalNone, Rows>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalNone, Rows>, grid, lds, s, rows, g, tbl);
   }
   return launched("encode_tail_kernel", grid, lds, s);
 }
@@ -784,15 +824,15 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
   switch (g.local_mode) {
     case kLocalXor:
       if (g.groups <= kMaxParkedLocals)
-        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, true, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        launch_lds(encode_kernel_asm<kLocalXor, true, Rows, NW>, grid, lds, s, rows, g, tbl);
       else
-        hipLaunchKernelGGL((encode_kernel_asm<kLocalXor, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+        launch_lds(encode_kernel_asm<kLocalXor, false, Rows, NW>, grid, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      hipLaunchKernelGGL((encode_kernel_asm<kLocalZero, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_kernel_asm<kLocalZero, false, Rows, NW>, grid, lds, s, rows, g, tbl);
       break;
     default:
-      hipLaunchKernelGGL((encode_kernel_asm<kLocalNone, false, Rows, NW>), grid, dim3(kBlock), lds, s, rows, g, tbl);
+      launch_lds(encode_kernel_asm<kLocalNone, false, Rows, NW>, grid, lds, s, rows, g, tbl);
   }
   return launched("encode_kernel_asm", grid, lds, s);
 }
@@ -896,8 +936,9 @@ hipError_t launch_encode_range(const Rows& rows, const EncodeGeom& g0, const uin
     g.tile_end = static_cast<uint32_t>(total);
     g.ticket = ticket;
     const dim3 grid(grid_for(total));
-    const hipError_t e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
-                                      : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+    const hipError_t e = g.nrows <= 4   ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+                         : g.nrows <= 8 ? launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s)
+                                        : launch_encode_asm<Rows, 4>(rows, g, tbl, grid, s);
     if (e != hipSuccess) return e;
   } else {
     for (uint64_t t0 = 0; t0 < total; t0 += win) {
@@ -907,15 +948,20 @@ hipError_t launch_encode_range(const Rows& rows, const EncodeGeom& g0, const uin
       const dim3 grid(grid_for(g.tile_end - g.tile_begin));
       hipError_t e;
       if (asm_tile)
-        e = g.nrows <= 4 ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
-                         : launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s);
+        e = g.nrows <= 4   ? launch_encode_asm<Rows, 1>(rows, g, tbl, grid, s)
+            : g.nrows <= 8 ? launch_encode_asm<Rows, 2>(rows, g, tbl, grid, s)
+                           : launch_encode_asm<Rows, 4>(rows, g, tbl, grid, s);
       else
-        e = g.nrows <= 4 ? launch_encode_nw<1>(rows, g, tbl, grid, s) : launch_encode_nw<2>(rows, g, tbl, grid, s);
+        e = g.nrows <= 4   ? launch_encode_nw<1>(rows, g, tbl, grid, s)
+            : g.nrows <= 8 ? launch_encode_nw<2>(rows, g, tbl, grid, s)
+                           : launch_encode_nw<4>(rows, g, tbl, grid, s);
       if (e != hipSuccess) return e;
     }
   }
   if (asm_tile && full < g0.tiles)
-    return g0.nrows <= 4 ? launch_encode_tail<Rows, 1>(rows, gw, tbl, s) : launch_encode_tail<Rows, 2>(rows, gw, tbl, s);
+    return g0.nrows <= 4   ? launch_encode_tail<Rows, 1>(rows, gw, tbl, s)
+           : g0.nrows <= 8 ? launch_encode_tail<Rows, 2>(rows, gw, tbl, s)
+                           : launch_encode_tail<Rows, 4>(rows, gw, tbl, s);
   return hipSuccess;
 }
 

@@ -172,13 +172,13 @@ class StripeSlab:
         return self.stripes * self.nblocks * self.len
 
     def encode_launches(self) -> int:
-        """Kernel launches one encode() makes: ceil(m / 8) row passes, each in
+        """Kernel launches one encode() makes: ceil(m / 16) row passes, each in
         windows of ENCODE_LAUNCH_TILES 4 KiB column tiles, or one ticket-ordered
         launch from TICKET_MIN_TILES tiles on (ecw_kernels.hip launch_encode).
         For per-launch timings next to rocprof's."""
         units, ulen = (self.units, self.chunk) if self.layout == "tiled" else (self.stripes, self.len)
         tiles = units * -(-ulen // 4096)
-        passes = max(1, -(-self.codec.scheme.globalParityNum // 8))
+        passes = max(1, -(-self.codec.scheme.globalParityNum // 16))  # kMaxPassRows
         if tiles >= TICKET_MIN_TILES and self.codec.encodeDataNum >= 2:
             return passes  # one ticket-ordered launch per pass
         return passes * -(-tiles // ENCODE_LAUNCH_TILES)

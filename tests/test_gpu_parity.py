@@ -736,16 +736,17 @@ def test_random_sweep_vs_oracle(E, torch, orc):
 
 
 @pytest.mark.parametrize("code,k,m,r,B,S", [
-    ("R", 128, 12, 0, 3 * 4096 + 80, 2),   # RS(128, 12): an 8-row and a 4-row pass
+    ("R", 128, 12, 0, 3 * 4096 + 80, 2),   # RS(128, 12): one pass of the 16-row asm tile + its ragged tail
     ("R", 20, 9, 0, 4096, 3),              # 9 rows
     ("C", 64, 16, 10, 8192 + 16, 2),       # 16 global rows + 7 XOR locals
-    ("C", 200, 10, 40, 4096 + 1, 1),       # wide k
-    ("R", 128, 20, 0, 4096, 1),            # 20 rows: 8 + 8 + 4
+    ("C", 200, 10, 40, 4096 + 1, 1),       # wide k: 100 KiB of tables (> 64 KiB of dynamic LDS)
+    ("C", 128, 9, 27, 8192, 3),            # 9 rows + 5 parked XOR locals
+    ("R", 128, 20, 0, 4096, 1),            # 20 rows: a 16-row pass and a 4-row pass
 ])
 def test_more_than_8_global_rows(E, torch, orc, code, k, m, r, B, S):
     """ECWide-C's RS / TL / CL codecs take any m (NativeCodec.java:20-54):
-    more than 8 global rows run in passes of <= 8 rows (a single-pass 16-row tile
-    measured slower: DESIGN.md section 5); slab mode, pointer mode
+    9-16 global rows run in ONE pass over the data (the 16-row asm tile:
+    16-byte packed entries, ds_read_b128), more in passes of 16; slab mode, pointer mode
     (blocks in reverse order) and device pointer tables, vs the oracle."""
     if code == "R":
         c = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(k, m, B))
