@@ -157,7 +157,7 @@ struct ecw_codec {
   std::vector<uint8_t> matrix;        // m x edn, row-major (encodeMatrix)
   std::vector<uint8_t> gftbl;         // 32 * edn * m (encodeGftbl, ISA-L layout)
   std::vector<uint8_t> dtbl, pdtbl;   // decode / partial-decode tables (all ones)
-  std::vector<std::vector<uint8_t>> pass_img;  // packed device tables per pass of <= 8 rows
+  std::vector<std::vector<uint8_t>> pass_img;  // packed device tables per pass of <= 16 rows
   bool xor_row = false;               // m == 1 and every coefficient 1: the global parity is a plain XOR
 
   std::mutex mu;                      // guards everything below

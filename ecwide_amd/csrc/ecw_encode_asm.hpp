@@ -1,6 +1,7 @@
 // Hand-scheduled encode of ONE full column tile (gfx950 / CDNA4), used by
 // encode_kernel_asm for every encode pass (slab or pointer mode; <= 4 global rows
-// below, 5-8 rows in the ECW2_* variant further down).
+// below, 5-8 rows in the ECW2_* variant and 9-16 rows in the ECW4_* variant
+// further down).
 //
 // Same arithmetic as encode_tile() in ecw_kernels.hip (ISA-L's 4-bit split
 // GF(2^8) products, gf_vect_mul_init, isal:erasure_code/ec_base.c:157-262,
