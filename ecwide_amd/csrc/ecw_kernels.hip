@@ -416,41 +416,53 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 #ifndef ECW_ASM_MIN_WAVES_NW4
 #define ECW_ASM_MIN_WAVES_NW4 3  // 168 VGPRs: the 16-row tile uses 142
 #endif
+#ifndef ECW_ASM_TPB4
+// 9-16 rows: workgroups of 2 tiles (512 threads) share one copy of the 64 KiB
+// (k = 128) tables, so the LDS holds tables for 16 waves per CU instead of 8
+#define ECW_ASM_TPB4 2
+#endif
+// column tiles per workgroup of the asm kernel (kBlock threads per tile)
+template <int NW>
+constexpr int asm_tpb() {
+  return NW == 4 ? ECW_ASM_TPB4 : 1;
+}
 
 // Copy the packed tables (n16 x 16 B) into LDS, four loads in flight per lane
 // (one at a time, each waited for before its LDS write, took four round trips
 // at k = 128).
+template <int NT = kBlock>
 __device__ __forceinline__ void stage_tables(uint8_t* lds, const uint4* __restrict__ tbl, int n16) {
   uint4* l4 = reinterpret_cast<uint4*>(lds);
   int i = threadIdx.x;
-  for (; i + 3 * kBlock < n16; i += 4 * kBlock) {
-    const uint4 a = tbl[i], b = tbl[i + kBlock], c = tbl[i + 2 * kBlock], d = tbl[i + 3 * kBlock];
+  for (; i + 3 * NT < n16; i += 4 * NT) {
+    const uint4 a = tbl[i], b = tbl[i + NT], c = tbl[i + 2 * NT], d = tbl[i + 3 * NT];
     l4[i] = a;
-    l4[i + kBlock] = b;
-    l4[i + 2 * kBlock] = c;
-    l4[i + 3 * kBlock] = d;
+    l4[i + NT] = b;
+    l4[i + 2 * NT] = c;
+    l4[i + 3 * NT] = d;
   }
-  for (; i < n16; i += kBlock) l4[i] = tbl[i];
+  for (; i < n16; i += NT) l4[i] = tbl[i];
 }
 
 // Next tile of a ticket-ordered launch (EncodeGeom::ticket): lane 0 of the
 // workgroup takes a ticket, the slot after the LDS tables hands it to the rest.
-__device__ __forceinline__ uint32_t take_ticket(const EncodeGeom& g, uint32_t* slot) {
+__device__ __forceinline__ uint32_t take_ticket(const EncodeGeom& g, uint32_t* slot, uint32_t tiles = 1) {
   __syncthreads();  // every wave has read the previous ticket
-  if (threadIdx.x == 0) *slot = g.tile_begin + static_cast<uint32_t>(atomicAdd(g.ticket, 1ull));
+  if (threadIdx.x == 0) *slot = g.tile_begin + static_cast<uint32_t>(atomicAdd(g.ticket, tiles));
   __syncthreads();
   return __builtin_amdgcn_readfirstlane(*slot);
 }
 
 template <int LOCAL, bool PARK, class Rows, int NW = 1>
-__global__ __launch_bounds__(kBlock, NW == 1   ? ECW_ASM_MIN_WAVES
-                                    : NW == 2 ? ECW_ASM_MIN_WAVES_NW2
-                                              : ECW_ASM_MIN_WAVES_NW4) void encode_kernel_asm(
+__global__ __launch_bounds__(kBlock * asm_tpb<NW>(), NW == 1   ? ECW_ASM_MIN_WAVES
+                                                   : NW == 2 ? ECW_ASM_MIN_WAVES_NW2
+                                                             : ECW_ASM_MIN_WAVES_NW4) void encode_kernel_asm(
     const Rows rows, const EncodeGeom g, const uint4* __restrict__ tbl) {
+  constexpr uint32_t TPB = asm_tpb<NW>();
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int n16 = g.k * 8 * NW;
 #ifndef ECW_DIAG_NOSTAGE  // diagnostic builds only: time the encode without staging its tables
-  stage_tables(lds, tbl, n16);
+  stage_tables<kBlock * TPB>(lds, tbl, n16);
   __syncthreads();
 #else
   (void)n16;
@@ -460,7 +472,10 @@ __global__ __launch_bounds__(kBlock, NW == 1   ? ECW_ASM_MIN_WAVES
   const int r = LOCAL == kLocalNone ? k : __builtin_amdgcn_readfirstlane(g.r);
   const int nrows = __builtin_amdgcn_readfirstlane(g.nrows);
   const uint32_t wmask = __builtin_amdgcn_readfirstlane(g.wmask), ww = __builtin_amdgcn_readfirstlane(g.wwidth);
-  const uint32_t lane_col = threadIdx.x * kLaneBytes;
+  // TPB > 1: waves [4h, 4h + 4) take tile h of the workgroup's TPB consecutive
+  // tiles (h is wave-uniform)
+  const uint32_t lane_col = (threadIdx.x % kBlock) * kLaneBytes;
+  const uint32_t half = __builtin_amdgcn_readfirstlane(threadIdx.x / kBlock);
   // the ticket slot sits after the tables: a static __shared__ variable would
   // shift the table records off the 64*NW alignment the LDS addressing relies on
   uint32_t* slot = reinterpret_cast<uint32_t*>(lds + static_cast<uint32_t>(g.k) * 128 * NW);
@@ -469,10 +484,14 @@ __global__ __launch_bounds__(kBlock, NW == 1   ? ECW_ASM_MIN_WAVES
   // last tile of every block is encode_tail_kernel's): nothing but the asm
   // tile and a few scalar instructions per tile, so nothing lives in scratch
   // and no compiler-issued memory operation drains the ring between tiles.
-  for (uint32_t tile = tickets ? take_ticket(g, slot) : g.tile_begin + static_cast<uint32_t>(wg_slot());
-       tile < g.tile_end; tile = tickets ? take_ticket(g, slot) : tile + gridDim.x) {
+  // Every wave runs every iteration (take_ticket holds a barrier); a wave whose
+  // tile is past the end skips the work.
+  for (uint32_t t0 = tickets ? take_ticket(g, slot, TPB) : g.tile_begin + static_cast<uint32_t>(wg_slot()) * TPB;
+       t0 < g.tile_end; t0 = tickets ? take_ticket(g, slot, TPB) : t0 + gridDim.x * TPB) {
+    const uint32_t tile = t0 + half;
+    if (tile >= g.tile_end) continue;
     const uint32_t s = fast_div(tile, g.per);
-    if (s >= static_cast<uint32_t>(g.stripes)) break;  // never past the batch, whatever the launch says
+    if (s >= static_cast<uint32_t>(g.stripes)) continue;  // never past the batch, whatever the launch says
     const uint32_t col = (tile - s * g.per.d) * kTileBytes + lane_col;
     if constexpr (std::is_same<Rows, SlabRows>::value) {
       const uint64_t bs = rows.bstride, pbs = rows.pbstride;
@@ -778,11 +797,11 @@ unsigned grid_for(uint64_t tiles_total, uint64_t per_cu = ECW_GRID_PER_CU) {
 // Launch with `lds` bytes of dynamic LDS; above 64 KiB (9-16-row tables of
 // wide stripes: k * 512 B) the kernel's limit is raised first (160 KiB per CU).
 template <class K, class... A>
-void launch_lds(K kernel, dim3 grid, size_t lds, hipStream_t s, const A&... a) {
+void launch_lds(K kernel, dim3 grid, unsigned threads, size_t lds, hipStream_t s, const A&... a) {
   if (lds > 65536)
     (void)hipFuncSetAttribute(reinterpret_cast<const void*>(kernel), hipFuncAttributeMaxDynamicSharedMemorySize,
                               static_cast<int>(lds));
-  hipLaunchKernelGGL(kernel, grid, dim3(kBlock), lds, s, a...);
+  hipLaunchKernelGGL(kernel, grid, dim3(threads), lds, s, a...);
 }
 
 template <int NW, class Rows>
@@ -790,13 +809,13 @@ hipError_t launch_encode_nw(const Rows& rows, const EncodeGeom& g, const uint4* 
   const size_t lds = static_cast<size_t>(g.k) * 128 * NW;
   switch (g.local_mode) {
     case kLocalXor:
-      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalXor, Rows>, grid, kBlock, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalZero, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalZero, Rows>, grid, kBlock, lds, s, rows, g, tbl);
       break;
     default:
-      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_kernel<NW, kPrefetchEnc, kLocalNone, Rows>, grid, kBlock, lds, s, rows, g, tbl);
   }
   return launched("encode_kernel", grid, lds, s);
 }
@@ -807,13 +826,13 @@ hipError_t launch_encode_tail(const Rows& rows, const EncodeGeom& g, const uint4
   const dim3 grid(static_cast<unsigned>(g.stripes < 65536 ? g.stripes : 65536));
   switch (g.local_mode) {
     case kLocalXor:
-      launch_lds(encode_tail_kernel<NW, kLocalXor, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalXor, Rows>, grid, kBlock, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      launch_lds(encode_tail_kernel<NW, kLocalZero, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalZero, Rows>, grid, kBlock, lds, s, rows, g, tbl);
       break;
     default:
-      launch_lds(encode_tail_kernel<NW, kLocalNone, Rows>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_tail_kernel<NW, kLocalNone, Rows>, grid, kBlock, lds, s, rows, g, tbl);
   }
   return launched("encode_tail_kernel", grid, lds, s);
 }
@@ -821,18 +840,21 @@ hipError_t launch_encode_tail(const Rows& rows, const EncodeGeom& g, const uint4
 template <class Rows, int NW>
 hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
   const size_t lds = static_cast<size_t>(g.k) * 128 * NW + 16;  // + ticket slot
+  constexpr unsigned TPB = asm_tpb<NW>();
+  const unsigned threads = kBlock * TPB;
+  grid.x = (grid.x + TPB - 1) / TPB;  // the launch's tiles in workgroups of TPB
   switch (g.local_mode) {
     case kLocalXor:
       if (g.groups <= kMaxParkedLocals)
-        launch_lds(encode_kernel_asm<kLocalXor, true, Rows, NW>, grid, lds, s, rows, g, tbl);
+        launch_lds(encode_kernel_asm<kLocalXor, true, Rows, NW>, grid, threads, lds, s, rows, g, tbl);
       else
-        launch_lds(encode_kernel_asm<kLocalXor, false, Rows, NW>, grid, lds, s, rows, g, tbl);
+        launch_lds(encode_kernel_asm<kLocalXor, false, Rows, NW>, grid, threads, lds, s, rows, g, tbl);
       break;
     case kLocalZero:
-      launch_lds(encode_kernel_asm<kLocalZero, false, Rows, NW>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_kernel_asm<kLocalZero, false, Rows, NW>, grid, threads, lds, s, rows, g, tbl);
       break;
     default:
-      launch_lds(encode_kernel_asm<kLocalNone, false, Rows, NW>, grid, lds, s, rows, g, tbl);
+      launch_lds(encode_kernel_asm<kLocalNone, false, Rows, NW>, grid, threads, lds, s, rows, g, tbl);
   }
   return launched("encode_kernel_asm", grid, lds, s);
 }
