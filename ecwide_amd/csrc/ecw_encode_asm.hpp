@@ -454,19 +454,23 @@
 
 // ---------------------------------------------------------------------------
 // 5-8 global rows (NW = 2): the same tile with one u64 table entry per nibble
-// (rows 0-3 in the low dword, 4-7 in the high one; records of 256 B, lo-nibble
-// entries at +0, hi at +128) and a second bank of packed accumulators.
-// Registers as above except: v33 = 0x78787878 (nibble * 8), lookup sets
-// v[42:57] / v[58:73] (eight even-aligned pairs each, the address in the low
-// register of its pair), accumulators of rows 4-7 in v[74:89], parked local
-// parities in v[90:109].
+// (rows 0-3 in the low dword, 4-7 in the high one; records of 256 B, hi- and
+// lo-nibble entries interleaved: hi of nibble n at +16n, lo at +16n + 8) and a
+// second bank of packed accumulators. The interleaving makes a hi address the
+// data byte's high nibble as it stands, so the nibble words cost one shift
+// instead of two; byte 0's addresses are built with v_bitop3 (2 cycles) instead
+// of v_perm (4): (word & 0xff) | the record address without its low byte.
+// Registers as above except: v33 = 0xF0F0F0F0 (nibble * 16), v41 = 0xff, s63
+// = the record address with its low byte cleared, lookup sets v[42:57] /
+// v[58:73] (eight even-aligned pairs each, the address in the low register of
+// its pair), accumulators of rows 4-7 in v[74:89], parked local parities in
+// v[90:109].
 #define ECW2_DW_ADDR(W, A0, A1, A2, A3, A4, A5, A6, A7) \
-  "v_lshlrev_b32 v34, 3, " W "\n\t"                     \
-  "v_lshrrev_b32 v35, 1, " W "\n\t"                     \
-  "v_and_or_b32 v34, v34, v33, s48\n\t"                 \
-  "v_and_or_b32 v35, v35, v33, s48\n\t"                 \
-  "v_perm_b32 " A0 ", v32, v34, s50\n\t"                \
-  "v_perm_b32 " A1 ", v32, v35, s50\n\t"                \
+  "v_lshlrev_b32 v34, 4, " W "\n\t"                     \
+  "v_bitop3_b32 v34, v34, v33, s48 bitop3:0xea\n\t"     \
+  "v_bitop3_b32 v35, " W ", v33, s48 bitop3:0xea\n\t"   \
+  "v_bitop3_b32 " A0 ", v34, v41, s63 bitop3:0xea\n\t"  \
+  "v_bitop3_b32 " A1 ", v35, v41, s63 bitop3:0xea\n\t"  \
   "v_perm_b32 " A2 ", v32, v34, s51\n\t"                \
   "v_perm_b32 " A3 ", v32, v35, s51\n\t"                \
   "v_perm_b32 " A4 ", v32, v34, s52\n\t"                \
@@ -476,23 +480,23 @@
 #define ECW2_ADDR_X(W) ECW2_DW_ADDR(W, "v42", "v44", "v46", "v48", "v50", "v52", "v54", "v56")
 #define ECW2_ADDR_Y(W) ECW2_DW_ADDR(W, "v58", "v60", "v62", "v64", "v66", "v68", "v70", "v72")
 #define ECW2_READ_X                                 \
-  "ds_read_b64 v[42:43], v42\n\t"                   \
-  "ds_read_b64 v[44:45], v44 offset:128\n\t"        \
-  "ds_read_b64 v[46:47], v46\n\t"                   \
-  "ds_read_b64 v[48:49], v48 offset:128\n\t"        \
-  "ds_read_b64 v[50:51], v50\n\t"                   \
-  "ds_read_b64 v[52:53], v52 offset:128\n\t"        \
-  "ds_read_b64 v[54:55], v54\n\t"                   \
-  "ds_read_b64 v[56:57], v56 offset:128\n\t"
+  "ds_read_b64 v[42:43], v42 offset:8\n\t"          \
+  "ds_read_b64 v[44:45], v44\n\t"                   \
+  "ds_read_b64 v[46:47], v46 offset:8\n\t"          \
+  "ds_read_b64 v[48:49], v48\n\t"                   \
+  "ds_read_b64 v[50:51], v50 offset:8\n\t"          \
+  "ds_read_b64 v[52:53], v52\n\t"                   \
+  "ds_read_b64 v[54:55], v54 offset:8\n\t"          \
+  "ds_read_b64 v[56:57], v56\n\t"
 #define ECW2_READ_Y                                 \
-  "ds_read_b64 v[58:59], v58\n\t"                   \
-  "ds_read_b64 v[60:61], v60 offset:128\n\t"        \
-  "ds_read_b64 v[62:63], v62\n\t"                   \
-  "ds_read_b64 v[64:65], v64 offset:128\n\t"        \
-  "ds_read_b64 v[66:67], v66\n\t"                   \
-  "ds_read_b64 v[68:69], v68 offset:128\n\t"        \
-  "ds_read_b64 v[70:71], v70\n\t"                   \
-  "ds_read_b64 v[72:73], v72 offset:128\n\t"
+  "ds_read_b64 v[58:59], v58 offset:8\n\t"          \
+  "ds_read_b64 v[60:61], v60\n\t"                   \
+  "ds_read_b64 v[62:63], v62 offset:8\n\t"          \
+  "ds_read_b64 v[64:65], v64\n\t"                   \
+  "ds_read_b64 v[66:67], v66 offset:8\n\t"          \
+  "ds_read_b64 v[68:69], v68\n\t"                   \
+  "ds_read_b64 v[70:71], v70 offset:8\n\t"          \
+  "ds_read_b64 v[72:73], v72\n\t"
 // byte b of the dword: lo-nibble pair (L, L+1), hi-nibble pair (H, H+1) into
 // accumulators C (rows 0-3) and D (rows 4-7)
 #define ECW2_FOLD1(C, D, L, L1, H, H1)                    \
@@ -517,6 +521,7 @@
 #define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
   "s_lshr_b32 s47, s46, 8\n\t"                                                         \
   "s_and_b32 s48, s46, 0xff\n\t"                                                       \
+  "s_andn2_b32 s63, s46, 0xff\n\t"                                                     \
   "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
   "v_mov_b32 v32, s47\n\t"                                                             \
   ECW2_ADDR_X(R0) ECW2_READ_X                                                          \
@@ -545,6 +550,7 @@
 #define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
   "s_lshr_b32 s47, s46, 8\n\t"                                                         \
   "s_and_b32 s48, s46, 0xff\n\t"                                                       \
+  "s_andn2_b32 s63, s46, 0xff\n\t"                                                     \
   "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
   "v_mov_b32 v32, s47\n\t"                                                             \
   ECW2_ADDR_X(R0) ECW2_READ_X                                                          \
@@ -617,7 +623,8 @@
 
 #define ECW2_TILE_ASM(BND, XL, END, MODE)                                          \
   "v_mov_b32 v40, %[col]\n\t"                                               \
-  "v_mov_b32 v33, 0x78787878\n\t"                                           \
+  "v_mov_b32 v33, 0xf0f0f0f0\n\t"                                           \
+  "v_mov_b32 v41, 0xff\n\t"                                                 \
   "s_mov_b32 s50, 0x0c0c0400\n\t"                                           \
   "s_mov_b32 s51, 0x0c0c0401\n\t"                                           \
   "s_mov_b32 s52, 0x0c0c0402\n\t"                                           \
@@ -707,7 +714,7 @@
   "31:"
 
 #define ECW2_TILE_OPERANDS                                                          \
-  ECW_TILE_OPERANDS, "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67",  \
+  ECW_TILE_OPERANDS, "s63", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67",  \
     "v68", "v69", "v70", "v71", "v72", "v73", "v74", "v75", "v76", "v77", "v78", "v79", "v80",      \
     "v81", "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89"
 #define ECW2_TILE_OPERANDS_PARK                                                     \

@@ -70,10 +70,13 @@ inline std::vector<uint8_t> isal_tables(int k, int rows, const uint8_t* a) {
 
 // Device table image for one pass of up to 16 global rows:
 // per data row j a record of 32 entries, entry type u32 (rows <= 4, NW = 1),
-// u64 (rows <= 8, NW = 2) or 16 bytes (rows <= 16, NW = 4). Entry n < 16 packs c_l * n of every row l of
-// the pass in byte l; entry 16 + n packs c_l * (n << 4). Record stride is
-// 128 * NW bytes, so the kernel's LDS address for (j, nibble) is
-// j * 128 * NW + nibble * 4 * NW (+ 64 * NW for the high nibble).
+// u64 (rows <= 8, NW = 2) or 16 bytes (rows <= 16, NW = 4). The lo entry of
+// nibble n packs c_l * n of every row l of the pass in byte l, the hi entry
+// c_l * (n << 4). Record stride is 128 * NW bytes. NW = 1 and 4: lo entries
+// first (address j * 128 * NW + n * 4 * NW), hi entries after them (+ 64 * NW).
+// NW = 2: hi and lo entries interleaved, hi at n * 16 and lo at n * 16 + 8, so
+// a hi address is the data byte's high nibble as it stands (W & 0xF0) and
+// costs no shift.
 inline std::vector<uint8_t> packed_pass_tables(const uint8_t* matrix, int k, int row0, int rows) {
   const int nw = rows <= 4 ? 1 : rows <= 8 ? 2 : 4;  // packed entry: 4, 8 or 16 bytes
   const size_t es = 4 * static_cast<size_t>(nw);
@@ -81,10 +84,11 @@ inline std::vector<uint8_t> packed_pass_tables(const uint8_t* matrix, int k, int
   for (int j = 0; j < k; ++j) {
     uint8_t* rec = img.data() + static_cast<size_t>(j) * 32 * es;
     for (int n = 0; n < 16; ++n) {
+      const size_t lo = nw == 2 ? (2 * n + 1) * es : n * es, hi = nw == 2 ? 2 * n * es : (16 + n) * es;
       for (int l = 0; l < rows; ++l) {
         const uint8_t c = matrix[static_cast<size_t>(row0 + l) * k + j];
-        rec[n * es + l] = gf_mul(c, static_cast<uint8_t>(n));
-        rec[(16 + n) * es + l] = gf_mul(c, static_cast<uint8_t>(n << 4));
+        rec[lo + l] = gf_mul(c, static_cast<uint8_t>(n));
+        rec[hi + l] = gf_mul(c, static_cast<uint8_t>(n << 4));
       }
     }
   }

@@ -185,12 +185,9 @@ __device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], 
   for (int d = 0; d < 4; ++d) {
     const uint32_t w = w4[d];
     // (nibble * entry size) in every byte, record low byte OR-ed in
-    const uint32_t lo = NW == 1   ? (((w << 2) & 0x3C3C3C3Cu) | jlo)
-                        : NW == 2 ? (((w << 3) & 0x78787878u) | jlo)
-                                  : (((w << 4) & 0xF0F0F0F0u) | jlo);
-    const uint32_t hi = NW == 1   ? (((w >> 2) & 0x3C3C3C3Cu) | jlo)
-                        : NW == 2 ? (((w >> 1) & 0x78787878u) | jlo)
-                                  : ((w & 0xF0F0F0F0u) | jlo);
+    // (NW = 2: lo entries at +8 of the interleaved pairs, ecw_gf.hpp)
+    const uint32_t lo = NW == 1 ? (((w << 2) & 0x3C3C3C3Cu) | jlo) : (((w << 4) & 0xF0F0F0F0u) | jlo);
+    const uint32_t hi = NW == 1 ? (((w >> 2) & 0x3C3C3C3Cu) | jlo) : ((w & 0xF0F0F0F0u) | jlo);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       // address = jhi << 8 | byte b of lo/hi  (selector: S1.byte b, S0.byte0,
@@ -204,8 +201,8 @@ __device__ __forceinline__ void gf_row(const uint4 x, uint32_t (&acc)[16 * NW], 
         const uint32_t th = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(ah + 64));
         acc[p] = xor3(acc[p], tl, th);
       } else if constexpr (NW == 2) {
-        const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al));
-        const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah + 128));
+        const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al + 8));
+        const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah));
         acc[2 * p] = xor3(acc[2 * p], static_cast<uint32_t>(tl), static_cast<uint32_t>(th));
         acc[2 * p + 1] = xor3(acc[2 * p + 1], static_cast<uint32_t>(tl >> 32), static_cast<uint32_t>(th >> 32));
       } else {
@@ -1129,8 +1126,9 @@ template <int NW>
 __device__ __forceinline__ void gf_dw(uint32_t w, uint32_t (&acc)[4 * NW], uint32_t rec) {
   const uint32_t jhi = rec >> 8;
   const uint32_t jlo = (rec & 0xFFu) * 0x01010101u;
-  const uint32_t lo = NW == 1 ? (((w << 2) & 0x3C3C3C3Cu) | jlo) : (((w << 3) & 0x78787878u) | jlo);
-  const uint32_t hi = NW == 1 ? (((w >> 2) & 0x3C3C3C3Cu) | jlo) : (((w >> 1) & 0x78787878u) | jlo);
+  // NW = 2: hi / lo entries interleaved (ecw_gf.hpp packed_pass_tables)
+  const uint32_t lo = NW == 1 ? (((w << 2) & 0x3C3C3C3Cu) | jlo) : (((w << 4) & 0xF0F0F0F0u) | jlo);
+  const uint32_t hi = NW == 1 ? (((w >> 2) & 0x3C3C3C3Cu) | jlo) : ((w & 0xF0F0F0F0u) | jlo);
 #pragma unroll
   for (int b = 0; b < 4; ++b) {
     const uint32_t sel = 0x0C0C0400u | static_cast<uint32_t>(b);
@@ -1141,8 +1139,8 @@ __device__ __forceinline__ void gf_dw(uint32_t w, uint32_t (&acc)[4 * NW], uint3
       const uint32_t th = *reinterpret_cast<lds_u32*>(static_cast<uintptr_t>(ah + 64));
       acc[b] = xor3(acc[b], tl, th);
     } else {
-      const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al));
-      const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah + 128));
+      const unsigned long long tl = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(al + 8));
+      const unsigned long long th = *reinterpret_cast<lds_u64*>(static_cast<uintptr_t>(ah));
       acc[2 * b] = xor3(acc[2 * b], static_cast<uint32_t>(tl), static_cast<uint32_t>(th));
       acc[2 * b + 1] = xor3(acc[2 * b + 1], static_cast<uint32_t>(tl >> 32), static_cast<uint32_t>(th >> 32));
     }
