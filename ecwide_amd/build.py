@@ -21,6 +21,12 @@ FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wal
          "-I" + os.path.join(REPO, "include")]
 
 
+def _tmp() -> str:
+    """Per-process temporary suffix: concurrent builders (pytest -n) never share
+    a half-written file; os.replace publishes the finished one atomically."""
+    return f".{os.getpid()}.tmp"
+
+
 def up_to_date(out=OUT, sources=SOURCES) -> bool:
     if not os.path.exists(out):
         return False
@@ -30,15 +36,15 @@ def up_to_date(out=OUT, sources=SOURCES) -> bool:
 
 def build(force: bool = False) -> str:
     if force or not up_to_date():
-        cmd = [HIPCC, *FLAGS, *SOURCES, "-o", OUT + ".tmp"]
+        cmd = [HIPCC, *FLAGS, *SOURCES, "-o", OUT + _tmp()]
         subprocess.run(cmd, check=True)
-        os.replace(OUT + ".tmp", OUT)
+        os.replace(OUT + _tmp(), OUT)
     if force or not up_to_date(SHIM_OUT, [SHIM_SRC, OUT]):
         # host-only C++; links libecwide.so next to it ($ORIGIN)
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + os.path.join(REPO, "include"),
-               SHIM_SRC, "-L" + HERE, "-lecwide", "-Wl,-rpath,$ORIGIN", "-o", SHIM_OUT + ".tmp"]
+               SHIM_SRC, "-L" + HERE, "-lecwide", "-Wl,-rpath,$ORIGIN", "-o", SHIM_OUT + _tmp()]
         subprocess.run(cmd, check=True)
-        os.replace(SHIM_OUT + ".tmp", SHIM_OUT)
+        os.replace(SHIM_OUT + _tmp(), SHIM_OUT)
     return OUT
 
 
@@ -69,9 +75,9 @@ def build_jni(include_dirs: list[str] | None = None, out: str = JNI_OUT, force: 
         rpath = os.path.relpath(HERE, os.path.dirname(os.path.abspath(out)))
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-fvisibility=hidden",
                *("-I" + d for d in include_dirs), "-I" + os.path.join(REPO, "include"), JNI_SRC,
-               "-L" + HERE, "-lecwide", "-Wl,-rpath,$ORIGIN/" + rpath, "-o", out + ".tmp"]
+               "-L" + HERE, "-lecwide", "-Wl,-rpath,$ORIGIN/" + rpath, "-o", out + _tmp()]
         subprocess.run(cmd, check=True)
-        os.replace(out + ".tmp", out)
+        os.replace(out + _tmp(), out)
     return out
 
 

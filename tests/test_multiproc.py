@@ -183,18 +183,21 @@ def test_bench_config_same_at_every_n():
     """SCALE's N=1 point is BENCH: the N=1 and N>1 lines carry the same
     `config` apart from stripes_total (n_gpus is top-level)."""
     lines = {}
-    for n in (1, 2, 4):
+    for n in (1, 2, 4, 8):
         p, line = _bench("--gpus", str(n), "--dry-run")
         assert p.returncode == 0, p.stderr[-2000:]
         lines[n] = line
     base = dict(lines[1]["config"])
     assert base["stripes_total"] == 8 and base["stripes_per_gpu"] == 8 and base["k"] == 128
     assert base["block_bytes"] == 64 << 20 and "per GPU" in base["workload"]
-    for n in (2, 4):
+    for n in (2, 4, 8):
         c = dict(lines[n]["config"])
         assert c.pop("stripes_total") == 8 * n
         assert c == {x: v for x, v in base.items() if x != "stripes_total"}
         assert lines[n]["n_gpus"] == n and lines[n]["scaling"] == "weak"
+        assert [x["s0"] for x in lines[n]["shares"]] == [8 * r for r in range(n)]
+        c4 = lines[n]["configs4"]  # the 256-stripe batch, split by stripe at every N
+        assert c4["stripes_total"] == 256 and sum(x["stripes"] for x in c4["shares"]) == 256
 
 
 def test_bench_dry_run_strong_and_column_modes():

@@ -40,8 +40,8 @@ def build() -> str:
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(obj, SOURCES))
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-Xarch_host", "-fsanitize=address", "-Xarch_host",
-                    "-fsanitize=undefined", *objs, "-lpthread", "-o", exe + ".tmp"], check=True)
-    os.replace(exe + ".tmp", exe)
+                    "-fsanitize=undefined", *objs, "-lpthread", "-o", exe + f".{os.getpid()}.tmp"], check=True)
+    os.replace(exe + f".{os.getpid()}.tmp", exe)
     return exe
 
 
