@@ -26,21 +26,49 @@ constexpr int kChains = 16;
 #define SDWA1(i) asm volatile("v_or_b32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:BYTE_1 src1_sel:DWORD" : "+v"(a[i]) : "v"(b));
 #define ANDOR1(i) asm volatile("v_and_or_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(sel));
 #define SHL1(i) asm volatile("v_lshlrev_b32 %0, 2, %0" : "+v"(a[i]));
+// wide lookups: 16 entries of W bytes at a stride of S bytes (ds_read_b64 /
+// b96 / b128), eight in flight per wave, the next address from the result
+#define WIDE8(INS, MASK, T)                                                                         \
+  {                                                                                                 \
+    T t0, t1, t2, t3, t4, t5, t6, t7;                                                               \
+    asm volatile("v_and_b32 %8, " MASK ", %8\n\t" INS " %0, %8\n\t"                                \
+                 "v_and_b32 %9, " MASK ", %9\n\t" INS " %1, %9\n\t"                                \
+                 "v_and_b32 %10, " MASK ", %10\n\t" INS " %2, %10\n\t"                             \
+                 "v_and_b32 %11, " MASK ", %11\n\t" INS " %3, %11\n\t"                             \
+                 "v_and_b32 %12, " MASK ", %12\n\t" INS " %4, %12\n\t"                             \
+                 "v_and_b32 %13, " MASK ", %13\n\t" INS " %5, %13\n\t"                             \
+                 "v_and_b32 %14, " MASK ", %14\n\t" INS " %6, %14\n\t"                             \
+                 "v_and_b32 %15, " MASK ", %15\n\t" INS " %7, %15\n\t"                             \
+                 "s_waitcnt lgkmcnt(0)"                                                             \
+                 : "=&v"(t0), "=&v"(t1), "=&v"(t2), "=&v"(t3), "=&v"(t4), "=&v"(t5), "=&v"(t6), "=&v"(t7), \
+                   "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]), "+v"(a[4]), "+v"(a[5]), "+v"(a[6]),   \
+                   "+v"(a[7])                                                                       \
+                 :                                                                                  \
+                 : "memory");                                                                       \
+    a[0] ^= t0.x; a[1] ^= t1.x; a[2] ^= t2.x; a[3] ^= t3.x;                                          \
+    a[4] ^= t4.x; a[5] ^= t5.x; a[6] ^= t6.x; a[7] ^= t7.x;                                          \
+  }
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
+typedef unsigned int v3u __attribute__((ext_vector_type(3)));
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
 #define X16(M) M(0) M(1) M(2) M(3) M(4) M(5) M(6) M(7) M(8) M(9) M(10) M(11) M(12) M(13) M(14) M(15)
 
 // MODE 0: v_perm_b32 only; 1: v_bitop3_b32 only; 2: ds_read_b32 (+ the
 // v_and forming its address); 3: the tile's mix per chain: 2 v_perm + 1 bitop3
 // + 1 ds_read_b32 (+ its v_and); 4: v_or_b32_sdwa (byte select); 5:
-// v_and_or_b32; 6: v_lshlrev_b32
+// v_and_or_b32; 6: v_lshlrev_b32; 7: ds_read_b64 (16 x 8 B); 8: ds_read_b96
+// (16 entries at a 16 B stride: the 9-16-row tile's record, 12 bytes used);
+// 9: ds_read_b128 (16 x 16 B) -- 7-9 each with a v_and and a v_xor per lookup
 template <int MODE>
 __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t seed) {
   __shared__ uint32_t tab[64];
-  if (threadIdx.x < 64) tab[threadIdx.x] = threadIdx.x * 0x01010101u;
+  if (threadIdx.x < 64) tab[threadIdx.x] = MODE >= 7 ? (threadIdx.x * 0x01010101u) & 0xF0F0F0F0u : threadIdx.x * 0x01010101u;
   __syncthreads();
   uint32_t a[kChains];
   const uint32_t b = seed ^ threadIdx.x, sel = 0x07050301u ^ (seed & 0x03030303u);
 #pragma unroll
-  for (int i = 0; i < kChains; ++i) a[i] = (threadIdx.x * 4 + i * 8) & 0x3c;
+  for (int i = 0; i < kChains; ++i)
+    a[i] = MODE == 7 ? (threadIdx.x * 8 + i * 24) & 0x78 : MODE >= 8 ? (threadIdx.x * 16 + i * 48) & 0xf0 : (threadIdx.x * 4 + i * 8) & 0x3c;
   const uint64_t t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
   for (int it = 0; it < iters; ++it) {
     if constexpr (MODE == 0) {
@@ -60,6 +88,15 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
       X16(ANDOR1)
     } else if constexpr (MODE == 6) {
       X16(SHL1)
+    } else if constexpr (MODE == 7) {
+      WIDE8("ds_read_b64", "0x78", v2u)
+      WIDE8("ds_read_b64", "0x78", v2u)
+    } else if constexpr (MODE == 8) {
+      WIDE8("ds_read_b96", "0xf0", v3u)
+      WIDE8("ds_read_b96", "0xf0", v3u)
+    } else if constexpr (MODE == 9) {
+      WIDE8("ds_read_b128", "0xf0", v4u)
+      WIDE8("ds_read_b128", "0xf0", v4u)
     } else {
       LDS1(0) LDS1(1) LDS1(2) LDS1(3) LDS1(4) LDS1(5) LDS1(6) LDS1(7)
       PERM1(8) PERM1(9) PERM1(10) PERM1(11) PERM1(12) PERM1(13) PERM1(14) PERM1(15)
@@ -88,10 +125,11 @@ __global__ __launch_bounds__(256) void bench(uint32_t* out, int iters, uint32_t 
 }
 
 // wave-instructions per iteration and mode: {VALU, LDS}
-static const int kValu[7] = {16, 16, 16, 16 + 32 + 16 + 16, 16, 16, 16};  // mix: 16 v_and + 32 perm + 16 bitop3 + 16 re-masks
-static const int kLds[7] = {0, 0, 16, 16, 0, 0, 0};
-static const char* kName[7] = {"v_perm_b32", "v_bitop3_b32", "ds_read_b32 (+v_and)", "mix 2 perm : 1 bitop3 : 1 lds",
-                               "v_or_b32_sdwa (BYTE_1)", "v_and_or_b32", "v_lshlrev_b32"};
+static const int kValu[10] = {16, 16, 16, 16 + 32 + 16 + 16, 16, 16, 16, 32, 32, 32};  // mix: 16 v_and + 32 perm + 16 bitop3 + 16 re-masks
+static const int kLds[10] = {0, 0, 16, 16, 0, 0, 0, 16, 16, 16};
+static const char* kName[10] = {"v_perm_b32", "v_bitop3_b32", "ds_read_b32 (+v_and)", "mix 2 perm : 1 bitop3 : 1 lds",
+                                "v_or_b32_sdwa (BYTE_1)", "v_and_or_b32", "v_lshlrev_b32",
+                                "ds_read_b64 (+v_and, v_xor)", "ds_read_b96 16B-stride (+2)", "ds_read_b128 (+2)"};
 
 template <int MODE>
 static void run(int blocks_per_cu, int cus, int iters) {
@@ -130,6 +168,15 @@ int main(int argc, char** argv) {
   CHECK(hipGetDevice(&dev));
   CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   std::printf("%d CUs, %d iterations\n", cus, iters);
+  if (argc > 2 && std::atoi(argv[2]) == 1) {  // the wide lookups only
+    for (int bpc : {1, 2, 4, 8}) {
+      run<2>(bpc, cus, iters);
+      run<7>(bpc, cus, iters);
+      run<8>(bpc, cus, iters);
+      run<9>(bpc, cus, iters);
+    }
+    return 0;
+  }
   for (int bpc : {1, 2, 4, 8}) {
     run<0>(bpc, cus, iters);
     run<1>(bpc, cus, iters);
