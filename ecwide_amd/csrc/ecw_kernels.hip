@@ -834,9 +834,13 @@ hipError_t launch_encode_tail(const Rows& rows, const EncodeGeom& g, const uint4
   return launched("encode_tail_kernel", grid, lds, s);
 }
 
+#ifndef ECW_ASM_LDS_PAD
+#define ECW_ASM_LDS_PAD 0
+#endif
 template <class Rows, int NW>
 hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4* tbl, dim3 grid, hipStream_t s) {
-  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + 16;  // + ticket slot
+  // + ticket slot (+ ECW_ASM_LDS_PAD: tuning builds only, fewer workgroups per CU)
+  const size_t lds = static_cast<size_t>(g.k) * 128 * NW + 16 + ECW_ASM_LDS_PAD;
   constexpr unsigned TPB = asm_tpb<NW>();
   const unsigned threads = kBlock * TPB;
   grid.x = (grid.x + TPB - 1) / TPB;  // the launch's tiles in workgroups of TPB
