@@ -418,10 +418,13 @@ __device__ __forceinline__ const uint8_t* uniform_ptr(const uint8_t* p) {
 // (k = 128) tables, so the LDS holds tables for 16 waves per CU instead of 8
 #define ECW_ASM_TPB4 2
 #endif
+#ifndef ECW_ASM_TPB1
+#define ECW_ASM_TPB1 1  // <= 4 rows (tuning: 2 = workgroups of two tiles sharing the 16 KiB of tables)
+#endif
 // column tiles per workgroup of the asm kernel (kBlock threads per tile)
 template <int NW>
 constexpr int asm_tpb() {
-  return NW == 4 ? ECW_ASM_TPB4 : 1;
+  return NW == 4 ? ECW_ASM_TPB4 : NW == 1 ? ECW_ASM_TPB1 : 1;
 }
 
 // Copy the packed tables (n16 x 16 B) into LDS, four loads in flight per lane
