@@ -20,4 +20,10 @@ cd $R
 timeout -k 10 600 python bench.py > $O/bench_default.log 2>&1 || exit $?
 tail -1 $O/bench_default.log | cut -c1-400
 find $O -name "*stats.csv" | head
+
+# the N = 2 path on this one GPU (self-launched ranks sharing the device)
+if [ -n "$WITH_2RANK" ]; then
+  timeout -k 10 900 python bench.py --gpus 2 > $O/bench_2rank_1gpu.log 2>&1 || { tail -20 $O/bench_2rank_1gpu.log; exit 1; }
+  tail -1 $O/bench_2rank_1gpu.log | cut -c1-400
+fi
 echo done
