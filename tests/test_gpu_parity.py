@@ -588,6 +588,20 @@ def test_decode_partial_xor_golden(E, torch, orc, manifest):
     assert np.array_equal(t, orc.xor_blocks(data))
     c.partialDecodeData(data[:4], t)
     assert np.array_equal(t, orc.xor_blocks(data[:4]))
+    # the same natives on HBM blocks (ecw_decode_dev / ecw_partial_decode_dev:
+    # the requestor's and a relayer's stage of the CL repair, ECTaskProcessor.java:
+    # 293-332), ragged length, against the oracle's decode over the codec's tables
+    oc = orc.codec("C", 128, 3, 27, 4096)
+    for ln in (4096, 3000, 17):
+        data = [orc.fill(ln, 51, 0, j) for j in range(9)]
+        d = dev_blocks(torch, 9, ln, data)
+        t = torch.zeros(ln, dtype=torch.uint8, device="cuda")
+        c.decodeData(d, t)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), oc.decode(data)), ln
+        c.partialDecodeData(d[:4], t)
+        torch.cuda.synchronize()
+        assert np.array_equal(t.cpu().numpy(), oc.partial_decode(data[:4])), ln
 
 
 def test_xor_intermediate_literal_and_xor(E, torch, orc, manifest):
