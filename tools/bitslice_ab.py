@@ -45,7 +45,8 @@ def main():
     assert L.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(h)) == 0
     mat = (ctypes.c_uint8 * (m * k))()
     assert L.ecw_codec_encode_matrix(h, mat, m * k) == 0
-    coef = [sum(mat[i * k + j] << (8 * i) for i in range(m)) for j in range(k)]
+    # 4 words per source: byte (i & 3) of word 4j + (i >> 2) = matrix[i][j]
+    coef = [sum(mat[i * k + j] << (8 * (i & 3)) for i in range(m) if i >> 2 == w) for j in range(k) for w in range(4)]
     coef_t = torch.tensor(coef, dtype=torch.int64).to(torch.int32).cuda()
     data = torch.empty(S * k * P, dtype=torch.uint8, device="cuda")
     par = torch.empty(S * (m + g) * P, dtype=torch.uint8, device="cuda")

@@ -46,7 +46,7 @@ __device__ __forceinline__ void stv(uint8_t* p, u32x4 v) { __builtin_nontemporal
 #endif
 
 template <int M>
-__device__ __forceinline__ void row(const u32x4& a, const u32x4& b, uint32_t cw, uint32_t (&lacc)[8],
+__device__ __forceinline__ void row(const u32x4& a, const u32x4& b, const uint32_t (&cw)[4], uint32_t (&lacc)[8],
                                     uint32_t (&acc)[M][8]) {
   uint32_t x[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
 #pragma unroll
@@ -55,7 +55,7 @@ __device__ __forceinline__ void row(const u32x4& a, const u32x4& b, uint32_t cw,
 #pragma unroll
   for (int r = 0; r < M; ++r)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) acc[r][i] += x[i] ^ cw;
+    for (int i = 0; i < 8; ++i) acc[r][i] += x[i] ^ cw[r >> 2];
 #else
   bs::transpose(x);
   uint32_t q[8][8];
@@ -64,14 +64,14 @@ __device__ __forceinline__ void row(const u32x4& a, const u32x4& b, uint32_t cw,
   // 2^3 x: fewer planes live at once than with all eight powers
   bs::powers_range<0, 4>(x, q);
 #pragma unroll
-  for (int r = 0; r < M; ++r) bs::apply<0>((cw >> (8 * r)) & 15u, acc[r], q);
+  for (int r = 0; r < M; ++r) bs::apply<0>((cw[r >> 2] >> (8 * (r & 3))) & 15u, acc[r], q);
   bs::powers_range<4, 8>(x, q);
 #pragma unroll
-  for (int r = 0; r < M; ++r) bs::apply<1>((cw >> (8 * r + 4)) & 15u, acc[r], q);
+  for (int r = 0; r < M; ++r) bs::apply<1>((cw[r >> 2] >> (8 * (r & 3) + 4)) & 15u, acc[r], q);
 #else
   bs::powers(x, q);
 #pragma unroll
-  for (int r = 0; r < M; ++r) bs::mul_acc((cw >> (8 * r)) & 255u, acc[r], q);
+  for (int r = 0; r < M; ++r) bs::mul_acc((cw[r >> 2] >> (8 * (r & 3))) & 255u, acc[r], q);
 #endif
 #endif
 }
@@ -117,7 +117,9 @@ __global__ __launch_bounds__(BS_TPB, BS_MINB) BS_WPE_ATTR void bs_encode_kernel(
   int gend = r < k ? r : k, grp = 0;
   for (int j = 0; j < k - 1; ++j) {
     const u32x4 na = BS_LD((j + 1) * kPiece + o1), nb = BS_LD((j + 1) * kPiece + o2);
-    const uint32_t cw = __builtin_amdgcn_readfirstlane(coef_t[j]);
+    uint32_t cw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) cw[w] = w * 4 < M ? __builtin_amdgcn_readfirstlane(coef_t[j * 4 + w]) : 0u;
     row<M>(ca, cb, cw, lacc, acc);
     if (g > 0 && j + 1 == gend) {
       park[(grp * 2 + 0) * kTpb + t] = u32x4{lacc[0], lacc[1], lacc[2], lacc[3]};
@@ -130,7 +132,12 @@ __global__ __launch_bounds__(BS_TPB, BS_MINB) BS_WPE_ATTR void bs_encode_kernel(
     ca = na;
     cb = nb;
   }
-  row<M>(ca, cb, __builtin_amdgcn_readfirstlane(coef_t[k - 1]), lacc, acc);
+  {
+    uint32_t cw[4];
+#pragma unroll
+    for (int w = 0; w < 4; ++w) cw[w] = w * 4 < M ? __builtin_amdgcn_readfirstlane(coef_t[(k - 1) * 4 + w]) : 0u;
+    row<M>(ca, cb, cw, lacc, acc);
+  }
   uint8_t* pb = parity + static_cast<size_t>(u) * (M + g) * kPiece;
 #pragma unroll
   for (int j = 0; j < M; ++j) {
@@ -151,18 +158,21 @@ __global__ __launch_bounds__(BS_TPB, BS_MINB) BS_WPE_ATTR void bs_encode_kernel(
 }  // namespace
 
 // data: units x k rows of 8 KiB; parity: units x (m + g) rows of 8 KiB;
-// coef_t (device): k words, byte r of word j = matrix[r][j]
+// coef_t (device): 4 words per source, byte (r & 3) of word 4j + (r >> 2) = matrix[r][j]
 extern "C" int bs_encode_split(const uint8_t* data, uint8_t* parity, const uint32_t* coef_t, int k, int m, int r,
                                int g, int units, void* stream) {
-  if (k < 1 || m < 1 || m > 4 || g < 0 || units < 1 || (g > 0 && r < 1)) return -1;
+  if (k < 1 || m < 1 || m > 16 || g < 0 || units < 1 || (g > 0 && r < 1)) return -1;
   const size_t lds = g > 1 ? static_cast<size_t>(g - 1) * 2 * kTpb * sizeof(u32x4) : 0;
   if (lds > 64 * 1024) return -2;
   hipStream_t s = static_cast<hipStream_t>(stream);
+#define BS_CASE(M_)                                                                                  \
+  case M_:                                                                                           \
+    hipLaunchKernelGGL(bs_encode_kernel<M_>, dim3(units * (kPiece / kTile)), dim3(kTpb), lds, s, data, parity, \
+                       coef_t, k, r, g);                                                             \
+    break;
   switch (m) {
-    case 1: hipLaunchKernelGGL(bs_encode_kernel<1>, dim3(units * (kPiece / kTile)), dim3(kTpb), lds, s, data, parity, coef_t, k, r, g); break;
-    case 2: hipLaunchKernelGGL(bs_encode_kernel<2>, dim3(units * (kPiece / kTile)), dim3(kTpb), lds, s, data, parity, coef_t, k, r, g); break;
-    case 3: hipLaunchKernelGGL(bs_encode_kernel<3>, dim3(units * (kPiece / kTile)), dim3(kTpb), lds, s, data, parity, coef_t, k, r, g); break;
-    default: hipLaunchKernelGGL(bs_encode_kernel<4>, dim3(units * (kPiece / kTile)), dim3(kTpb), lds, s, data, parity, coef_t, k, r, g); break;
+    BS_CASE(1) BS_CASE(2) BS_CASE(3) BS_CASE(4) BS_CASE(5) BS_CASE(8) BS_CASE(10) BS_CASE(12) BS_CASE(16)
+    default: return -4;
   }
   return hipGetLastError() == hipSuccess ? 0 : -3;
 }
