@@ -5,9 +5,9 @@ product is ``libecwide.so`` (HIP kernels for gfx950 behind the C ABI in
 include/ecwide.h); this package is its host-side mirror of the reference's
 CodingScheme / NativeCodec interface plus the HBM stripe-slab batch API.
 """
-from .codec import BlockBatch, CodingScheme, EcwError, NativeCodec, device_count, xor_reduce  # noqa: F401
+from .codec import BlockBatch, CodingScheme, EcwError, NativeCodec, device_count, service_counters, xor_reduce  # noqa: F401
 from .slab import StripeSlab  # noqa: F401
 from ._lib import LIB_PATH, lib  # noqa: F401
 
-__all__ = ["CodingScheme", "NativeCodec", "EcwError", "StripeSlab", "BlockBatch", "xor_reduce", "device_count",
+__all__ = ["CodingScheme", "NativeCodec", "EcwError", "StripeSlab", "BlockBatch", "xor_reduce", "device_count", "service_counters",
            "LIB_PATH"]

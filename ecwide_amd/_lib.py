@@ -90,6 +90,7 @@ SIGNATURES = {
     "ecw_repair_batch_dev": (c_int, [c_void_p, c_void_p, c_size_t, c_size_t, c_int, c_int, c_void_p, c_size_t,
                                      c_size_t, c_void_p]),
     "ecw_repair_sources": (c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
+    "ecw_service_counters": (c_int, [c_int, POINTER(c_uint64)]),
     "ecw_fill_random_dev": (c_int, [c_int, c_void_p, c_size_t, c_size_t, c_int, c_int, c_size_t, c_uint64, c_int,
                                     c_int, c_void_p]),
     "ecw_fill_random_pieces_dev": (c_int, [c_int, c_void_p, c_size_t, c_size_t, c_int, c_int, c_size_t, c_size_t,

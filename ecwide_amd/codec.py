@@ -16,7 +16,7 @@ shared between codecs; local parities are XOR by default (``local_mode``
 from __future__ import annotations
 
 import ctypes
-from ctypes import byref, c_int, c_void_p
+from ctypes import byref, c_int, c_uint64, c_void_p
 
 import numpy as np
 
@@ -352,3 +352,12 @@ def xor_reduce(src, dst, length=None, device: int = 0) -> None:
 
 def device_count() -> int:
     return lib.ecw_device_count()
+
+
+def service_counters(device: int = 0) -> dict:
+    """The resident small-request service's counters on `device`
+    (ecw_service_counters): requests served, eligible requests that took the
+    launch path, epochs launched, and whether it turned itself off."""
+    out = (c_uint64 * 4)()
+    _check(lib.ecw_service_counters(device, out), "service_counters")
+    return {"served": out[0], "declined": out[1], "epochs": out[2], "broken": bool(out[3])}

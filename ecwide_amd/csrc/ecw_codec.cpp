@@ -62,6 +62,9 @@ bool busy(int device);  // the request service's resident kernel is (or may be) 
 // for its own work in between).
 void yield(int device, bool hold);
 void release_hold(int device);
+constexpr int kNotServed = 1;  // not an error: the caller takes the launch path
+// serve one small request through the resident kernel (below), or kNotServed
+int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8_t* const* parity, size_t len, bool xor_only);
 // RAII form for the blocking host-memory entry points
 struct Hold {
   int device;
@@ -80,8 +83,10 @@ struct Hold {
 // which it does not while the request service's resident kernel serves other
 // threads (up to its lifetime). Codec teardown and staging growth therefore
 // hand their old allocations to this list while the service runs; they are
-// released by the first codec create / destroy / staging growth that finds
-// the service gone, and at process exit.
+// released by the next release that finds the service gone, and by the
+// service itself whenever an epoch has left and before it launches the next
+// (svc::Service::ensure_running), so the list holds at most what one epoch's
+// lifetime (100 ms) of teardowns deferred.
 namespace grave {
 
 enum Kind { kDevice, kHost, kStream, kEvent };
@@ -103,15 +108,33 @@ void release_now(const Item& it) {
   }
 }
 
-// release everything of devices whose service is not running
+// release everything of devices whose service is not running (svc::busy takes
+// the service's lock: never called with `mu` held, the service calls
+// reap_device with its own lock held)
 void reap() {
-  std::vector<Item> now;
+  std::vector<Item> all, keep, now;
   {
     std::lock_guard<std::mutex> lk(mu);
     if (items.empty()) return;
-    std::vector<Item> keep;
-    for (const Item& it : items) (svc::busy(it.device) ? keep : now).push_back(it);
-    items.swap(keep);
+    all.swap(items);
+  }
+  for (const Item& it : all) (svc::busy(it.device) ? keep : now).push_back(it);
+  if (!keep.empty()) {
+    std::lock_guard<std::mutex> lk(mu);
+    items.insert(items.end(), keep.begin(), keep.end());
+  }
+  for (const Item& it : now) release_now(it);
+}
+
+// release everything of `device`: its service has left and is not relaunched
+// meanwhile (the caller holds the service's lock)
+void reap_device(int device) {
+  std::vector<Item> now;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto mid = std::stable_partition(items.begin(), items.end(), [&](const Item& it) { return it.device != device; });
+    now.assign(mid, items.end());
+    items.erase(mid, items.end());
   }
   for (const Item& it : now) release_now(it);
 }
@@ -1037,6 +1060,7 @@ static int drain(HostPipe& P, int st) {
 }
 
 typedef int (*host_op)(ecw_codec*, uint8_t* const*, int, uint8_t* const*, int, size_t, hipStream_t);
+static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout, int, size_t len, hipStream_t s);
 
 static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8_t* const* out, int nout,
                           size_t len, host_op op) {
@@ -1045,12 +1069,22 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
   for (int i = 0; i < nout; ++i)
     if (!out[i]) return ECW_EINVAL;
   if (len == 0) return ECW_OK;
+  // a small XOR (decodeData / partialDecodeData / repair / xorIntemediate of
+  // blocks up to 64 KiB): the resident request service, no launch
+  const bool small = len <= kSvcMaxLen;
+  if (small && op == op_xor && nout == 1) {
+    const int sst = svc::serve(c, in, nin, out, len, true);
+    if (sst != svc::kNotServed) return sst;
+  }
   std::lock_guard<std::mutex> lk(c->mu);
   int st = c->ensure_device();
   if (st) return st;
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
-  svc::Hold hold(c->device);  // not queued behind the request service's resident kernel
+  // bulk work is not queued behind the request service's resident kernel (its
+  // launches also ask a running epoch to leave); a small call the service did
+  // not take does not hold it off in turn
+  svc::Hold hold(c->device, !small);
   if (!c->pipe) {
     c->pipe = new (std::nothrow) HostPipe();
     if (!c->pipe) return ECW_ENOMEM;
@@ -1117,8 +1151,6 @@ static int op_xor(ecw_codec*, uint8_t* const* din, int nin, uint8_t* const* dout
 // request on any slot. ECW_SERVICE=0 turns the service off.
 namespace svc {
 
-constexpr int kNotServed = 1;  // not an error: the caller takes the launch path
-
 bool enabled() {
   static const bool on = [] {
     const char* e = std::getenv("ECW_SERVICE");
@@ -1143,6 +1175,7 @@ struct Service {
   // any, the resident kernel is not relaunched and new small calls take the
   // launch path, so that work never queues behind it
   std::atomic<int> holds{0};
+  std::atomic<unsigned long long> n_served{0}, n_declined{0};  // ecw_service_counters
   uint8_t* stage[kSvcSlots] = {};
   uint8_t* d_stage[kSvcSlots] = {};
   size_t stage_bytes[kSvcSlots] = {};
@@ -1186,6 +1219,7 @@ struct Service {
   int ensure_running() {
     if (epoch != 0 && __atomic_load_n(&ctl->exited_epoch, __ATOMIC_ACQUIRE) != epoch) return ECW_OK;
     if (holds.load(std::memory_order_acquire) > 0) return ECW_OK;  // relaunched once the hold ends
+    grave::reap_device(device);  // what teardowns deferred while the last epoch ran
     __atomic_store_n(&ctl->stop, 0ull, __ATOMIC_RELEASE);  // a yield asked the previous epoch to leave
     DeviceGuard g(device);
     if (!g.ok || hipMemsetAsync(d_state, 0, sizeof(SvcDev), stream) != hipSuccess) return ECW_EDEVICE;
@@ -1303,30 +1337,38 @@ Service* service_for(int device) {
   return sv;
 }
 
-// Serve one stripe, or return kNotServed (shape or state not suitable).
-int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
-  const int k = c->k(), m = c->m(), np = c->info.parity_num;
+// Serve one request, or return kNotServed (shape or state not suitable): the
+// codec's encode of one stripe (xor_only false: k data blocks -> its parity
+// blocks), or the XOR of `nsrc` blocks into one (xor_only true: decodeData /
+// partialDecodeData / a CL repair / xorIntemediate on host memory; no tables).
+extern "C++" int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8_t* const* parity, size_t len,
+                       bool xor_only) {
+  const int k = xor_only ? nsrc : c->k(), m = xor_only ? 1 : c->m(), np = xor_only ? 1 : c->info.parity_num;
   const int nw = m <= 4 ? 1 : 2;
-  if (!enabled() || m < 1 || m > kMaxSvcRows || len == 0 || len > kSvcMaxLen ||
-      static_cast<size_t>(k) * 128 * nw > kSvcLds)
+  if (!enabled() || m < 1 || m > kMaxSvcRows || len == 0 || len > kSvcMaxLen || k < 1 || k > kMaxSrc ||
+      (!xor_only && static_cast<size_t>(k) * 128 * nw > kSvcLds))
     return kNotServed;
   {
     std::lock_guard<std::mutex> lk(c->mu);
     if (c->ensure_device() != ECW_OK) return kNotServed;  // the launch path reports the error
   }
   Service* sv = service_for(c->device);
-  if (sv->holds.load(std::memory_order_acquire) > 0) return kNotServed;  // launch-path work in flight
+  auto decline = [&] {
+    sv->n_declined.fetch_add(1, std::memory_order_relaxed);
+    return kNotServed;
+  };
+  if (sv->holds.load(std::memory_order_acquire) > 0) return decline();  // launch-path work in flight
   const size_t cs = (len + 255) & ~static_cast<size_t>(255);
   int slot;
   {
     std::unique_lock<std::mutex> lk(sv->mu);
-    if (sv->broken) return kNotServed;
+    if (sv->broken) return decline();
     if (!sv->ctl && sv->init() != ECW_OK) {
       sv->broken = true;
-      return kNotServed;
+      return decline();
     }
     sv->cv.wait(lk, [&] { return !sv->free_slots.empty() || sv->broken; });
-    if (sv->broken) return kNotServed;
+    if (sv->broken) return decline();
     // a thread keeps the slot it had last time when it is free: its parts
     // poll at full speed (a slot idle for 1 ms polls slowly) and may still
     // hold the thread's request words and tables
@@ -1339,7 +1381,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     if (sv->ensure_stage(slot, cs * (k + np)) != ECW_OK) {
       sv->free_slots.push_back(slot);
       sv->cv.notify_one();
-      return kNotServed;
+      return decline();
     }
   }
   // give the slot back (takes mu: never call it with mu held)
@@ -1369,11 +1411,11 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     w.k = k;
     w.nrows = m;
     w.m = m;
-    w.r = c->has_local() ? c->r() : k;
-    w.groups = c->groups();
-    w.local_mode = local_mode_of(c);
+    w.r = !xor_only && c->has_local() ? c->r() : k;
+    w.groups = xor_only ? 0 : c->groups();
+    w.local_mode = xor_only ? kLocalNone : local_mode_of(c);
     w.nw = nw;
-    w.flags = c->xor_row ? kSvcXorRow : 0;
+    w.flags = xor_only || c->xor_row ? kSvcXorRow : 0;  // a plain XOR: no tables staged
     w.serial = c->serial;
     return w;
   }();
@@ -1385,6 +1427,7 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
   }
   const unsigned long long units = (len + kSvcThreads * 4 - 1) / (kSvcThreads * 4);
   const int active = static_cast<int>(std::min<unsigned long long>(units, kSvcParts));
+  const unsigned long long prev_seq = q.seq;
   const unsigned long long seq = (gen << kSvcSeqBits) | (static_cast<unsigned long long>(active) << 32) |
                                  (((q.seq & kSvcReqMask) + 1) & kSvcReqMask);
   __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
@@ -1394,10 +1437,13 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     up = sv->ensure_running() == ECW_OK;
     if (!up) sv->broken = true;  // the launch path takes this call and every later one
   }
-  if (!up) return release(kNotServed);
+  if (!up) {
+    release(0);
+    return decline();
+  }
   const auto t0 = std::chrono::steady_clock::now();
   int failed = ECW_OK;
-  bool timed_out = false;
+  bool timed_out = false, held_off = false;
   // every part with work publishes its own done word (one cache line)
   auto finished = [&] {
     for (int p = 0; p < active; ++p)
@@ -1417,6 +1463,18 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
       failed = ECW_EDEVICE;
       break;
     }
+    // The epoch left without serving this request (a launch-path call asked it
+    // to) and a hold keeps the next one from starting: take the launch path
+    // now instead of waiting for every hold to end. The service stays on. No
+    // kernel polls while the epoch is gone and none starts while mu is held,
+    // so the request is withdrawn (the slot's word restored) before the slot
+    // is given back.
+    if (sv->holds.load(std::memory_order_acquire) > 0 &&
+        __atomic_load_n(&sv->ctl->exited_epoch, __ATOMIC_ACQUIRE) == sv->epoch) {
+      __atomic_store_n(&q.seq, prev_seq, __ATOMIC_RELEASE);
+      held_off = true;
+      break;
+    }
     if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(10)) {
       // Not served in 10 s. An epoch that has not started is queued behind
       // other work on the device (contention): this call takes the launch path
@@ -1429,7 +1487,10 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     }
   }
   if (failed) return release(failed);
-  if (timed_out) return release(kNotServed);
+  if (timed_out || held_off) {
+    release(0);
+    return decline();
+  }
 #if ECW_SVC_TRACE
   const auto tr2 = std::chrono::steady_clock::now();
 #endif
@@ -1446,10 +1507,30 @@ int encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, siz
     ++g_tr_n;
   }
 #endif
+  sv->n_served.fetch_add(1, std::memory_order_relaxed);
   return release(ECW_OK);
 }
 
+extern "C++" int counters(int device, unsigned long long out[4]) {
+  Service* sv = find(device);
+  if (!sv) {
+    for (int i = 0; i < 4; ++i) out[i] = 0;
+    return ECW_OK;
+  }
+  std::lock_guard<std::mutex> lk(sv->mu);
+  out[0] = sv->n_served.load(std::memory_order_relaxed);
+  out[1] = sv->n_declined.load(std::memory_order_relaxed);
+  out[2] = sv->epoch;
+  out[3] = sv->broken ? 1 : 0;
+  return ECW_OK;
+}
+
 }  // namespace svc
+
+int ecw_service_counters(int device, unsigned long long out[4]) {
+  if (!out || device < 0) return ECW_EINVAL;
+  return svc::counters(device, out);
+}
 
 int ecw_encode(ecw_codec* c, const uint8_t* const* data, uint8_t* const* parity, size_t len) {
   if (!c || !data || !parity || !check_len(len)) return ECW_EINVAL;
@@ -1592,7 +1673,7 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
     if (!parity[i]) return ECW_EINVAL;
   if (len == 0 || stripes == 0) return ECW_OK;
   if (stripes == 1 && len <= kSvcMaxLen) {
-    const int sst = svc::encode(c, data, parity, len);
+    const int sst = svc::serve(c, data, c->k(), parity, len, false);
     if (sst != svc::kNotServed) return sst;
   }
   std::lock_guard<std::mutex> lk(c->mu);

@@ -141,6 +141,14 @@ struct XorGeom {
   uint64_t len, tiles;
   int stripes, n;
 };
+// Set by the XOR launcher (ecw_kernels.hip launch_xor_range): the kernel's
+// unit is a group of K column tiles (K a template argument of the kernel).
+struct XorSched {
+  FastDiv per;            // column groups per stripe
+  FastDiv ns;             // stripes (order 1)
+  uint32_t order;         // 0: groups numbered stripe-major, 1: column-major
+  uint32_t wmask, wwidth; // write window: store when (clock & wmask) < wwidth; 0 = off
+};
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_split(const XorSplit& p, const XorGeom& g, hipStream_t s);

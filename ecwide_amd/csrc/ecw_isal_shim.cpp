@@ -14,7 +14,7 @@
 //
 // ECWide-H calls ec_encode_data on 4 KiB chunks from four proxy threads
 // (ECWide-H/proxy/proxy.cpp:2001-2012). Each call is one synchronous request
-// to libecwide's resident request service (ecw_encode -> svc::encode), which
+// to libecwide's resident request service (ecw_encode -> svc::serve), which
 // serves concurrent callers on separate slots. With the service off
 // (ECW_SERVICE=0) one GPU round trip costs far more than 4 KiB of work, so
 // concurrent callers are batched instead (group commit): a call joins the

@@ -618,49 +618,99 @@ __global__ __launch_bounds__(kBlock) void xor_kernel(const Args a, const XorGeom
 #ifndef ECW_XOR_WINDOW
 #define ECW_XOR_WINDOW 8
 #endif
-template <int N, bool TAIL, class Args>
-__device__ __forceinline__ void xor_tile_fixed(const Args& a, const XorGeom& g, int s, uint32_t col) {
+// Write window of the XOR reduce (XorSched::wwidth > 0): the output store
+// waits until the chip-wide 100 MHz constant clock is in the first `wwidth`
+// ticks of every `wmask + 1`, as the encode's asm tile does
+// (ECW_WRITE_WINDOW, ecw_encode_asm.hpp); at most 16384 polls.
+__device__ __forceinline__ void xor_write_window(uint32_t wmask, uint32_t wwidth) {
+  if (wwidth == 0) return;
+#pragma nounroll
+  for (int n = 0; n < 16384; ++n) {
+    const uint32_t t = static_cast<uint32_t>(__builtin_amdgcn_s_memrealtime());
+    if ((t & wmask) < wwidth) break;
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// One workgroup reduces K consecutive column tiles of one stripe. K = 1 is
+// the plain tile. K > 1 skews the schedule diagonally: load t of the
+// straight-line sequence reads source i = t % N at tile (t / N + i) % K, so
+// the loads a wave has in flight (and the loads of the workgroups that run
+// beside it) fall on K different column tiles of the sources instead of one.
+// Blocks allocated separately start at the same offset modulo every large
+// power of two, so one column of all n sources can sit on one HBM channel and
+// bank, a row apart (SURVEY §7 "channel camping"; the slabs avoid it with a
+// +4 KiB block stride, which the reference's per-block buffers,
+// NativeCodec.cc:237-248, do not have).
+template <int N, int K, bool TAIL, class Args>
+__device__ __forceinline__ void xor_tiles_fixed(const Args& a, const XorGeom& g, const XorSched& sc, int s,
+                                                uint32_t col) {
   const uint32_t len = static_cast<uint32_t>(g.len);
   if (TAIL && col >= len) return;
-  constexpr int W = ECW_XOR_WINDOW > 0 && ECW_XOR_WINDOW < N ? ECW_XOR_WINDOW : N;
-  uint4 v[N];
-  uint4 acc = make_uint4(0, 0, 0, 0);
-  // pointer tables: every source pointer first (one batch of scalar loads)
-  const uint8_t* sp[std::is_same<Args, XorTab>::value ? N : 1];
-  if constexpr (std::is_same<Args, XorTab>::value) {
+  constexpr int T = N * K;
+  constexpr int W = ECW_XOR_WINDOW > 0 && ECW_XOR_WINDOW < T ? ECW_XOR_WINDOW : T;
+  uint4 v[T];
+  uint4 acc[K];
 #pragma unroll
-    for (int i = 0; i < N; ++i) sp[i] = xsrc(a, s, i);
-  }
+  for (int q = 0; q < K; ++q) acc[q] = make_uint4(0, 0, 0, 0);
+  // every source pointer first (pointer tables: one batch of scalar loads)
+  const uint8_t* sp[N];
+#pragma unroll
+  for (int i = 0; i < N; ++i) sp[i] = xsrc(a, s, i);
   // the scheduling barriers pin the issue order (the machine scheduler would
   // otherwise pull the first XORs up between the first loads: vmcnt(0) after two)
 #pragma unroll
-  for (int i = 0; i < N; ++i) {
-    if constexpr (std::is_same<Args, XorTab>::value)
-      v[i] = ld16<TAIL, ECW_XOR_NT>(sp[i], col, len);
-    else
-      v[i] = ld16<TAIL, ECW_XOR_NT>(xsrc(a, s, i), col, len);
+  for (int t = 0; t < T; ++t) {
+    v[t] = ld16<TAIL, ECW_XOR_NT>(sp[t % N], col + ((t / N + t % N) % K) * kTileBytes, len);
     __builtin_amdgcn_sched_barrier(0);
-    if (i >= W - 1) {
-      acc = xor4(acc, v[i - W + 1]);
-      if (W < N) asm volatile("" : "+v"(acc.x), "+v"(acc.y), "+v"(acc.z), "+v"(acc.w));  // keep the XOR here
+    if (t >= W - 1) {
+      const int u = t - W + 1;
+      uint4& ac = acc[(u / N + u % N) % K];
+      ac = xor4(ac, v[u]);
+      if (W < T) asm volatile("" : "+v"(ac.x), "+v"(ac.y), "+v"(ac.z), "+v"(ac.w));  // keep the XOR here
     }
   }
 #pragma unroll
-  for (int i = N - W + 1; i < N; ++i) acc = xor4(acc, v[i]);
-  st16<TAIL, ECW_XOR_NT>(xdst(a, s), col, len, acc);
+  for (int u = T - W + 1; u < T; ++u) {
+    uint4& ac = acc[(u / N + u % N) % K];
+    ac = xor4(ac, v[u]);
+  }
+  xor_write_window(sc.wmask, sc.wwidth);
+  uint8_t* d = xdst(a, s);
+#pragma unroll
+  for (int q = 0; q < K; ++q) st16<TAIL, ECW_XOR_NT>(d, col + q * kTileBytes, len, acc[q]);
 }
 
-template <int N, class Args>
-__global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g, const FastDiv per) {
-  const uint32_t total = static_cast<uint32_t>(g.stripes) * per.d;
-  for (uint32_t tile = static_cast<uint32_t>(wg_slot()); tile < total; tile += gridDim.x) {
-    const int s = static_cast<int>(fast_div(tile, per));
-    const uint32_t col0 = (tile - static_cast<uint32_t>(s) * per.d) * kTileBytes;
+// Groups of K column tiles, numbered stripe-major (order 0: group = stripe *
+// per + column group) or column-major (order 1: group = column group *
+// stripes + stripe, so the workgroups in flight spread over every stripe).
+template <int N, int K, class Args>
+__global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g, const XorSched sc) {
+  const uint32_t total = static_cast<uint32_t>(g.stripes) * sc.per.d;
+  for (uint32_t grp = static_cast<uint32_t>(wg_slot()); grp < total; grp += gridDim.x) {
+    uint32_t s, c;
+    if (sc.order) {
+      c = fast_div(grp, sc.ns);
+      s = grp - c * sc.ns.d;
+    } else {
+      s = fast_div(grp, sc.per);
+      c = grp - s * sc.per.d;
+    }
+    const uint32_t col0 = c * (K * kTileBytes);
     const uint32_t col = col0 + threadIdx.x * kLaneBytes;
-    if (static_cast<uint64_t>(col0) + kTileBytes <= g.len)
-      xor_tile_fixed<N, false>(a, g, s, col);
-    else
-      xor_tile_fixed<N, true>(a, g, s, col);
+    if (static_cast<uint64_t>(col0) + K * kTileBytes <= g.len) {
+      xor_tiles_fixed<N, K, false>(a, g, sc, static_cast<int>(s), col);
+    } else {
+      // the ragged last group of a stripe: its tiles one by one
+      for (uint32_t q = 0; q < static_cast<uint32_t>(K); ++q) {
+        const uint32_t c0 = col0 + q * kTileBytes;
+        if (c0 >= g.len) break;
+        if (static_cast<uint64_t>(c0) + kTileBytes <= g.len)
+          xor_tiles_fixed<N, 1, false>(a, g, sc, static_cast<int>(s), col + q * kTileBytes);
+        else
+          xor_tiles_fixed<N, 1, true>(a, g, sc, static_cast<int>(s), col + q * kTileBytes);
+      }
+    }
   }
 }
 
@@ -1011,14 +1061,70 @@ hipError_t launch_encode(const Rows& rows, const EncodeGeom& g0, const void* d_t
   return hipSuccess;
 }
 
-template <int N, class Args>
-hipError_t launch_xor_fixed(const Args& a, const XorGeom& g, const FastDiv& per, dim3 grid, hipStream_t s) {
+template <int N, int K, class Args>
+hipError_t launch_xor_fixed(const Args& a, const XorGeom& g, const XorSched& sc, dim3 grid, hipStream_t s) {
   if constexpr (N >= 1) {
-    if (g.n < N) return launch_xor_fixed<N - 1>(a, g, per, grid, s);
-    hipLaunchKernelGGL((xor_kernel_fixed<N, Args>), grid, dim3(kBlock), 0, s, a, g, per);
+    if (g.n < N) return launch_xor_fixed<N - 1, K>(a, g, sc, grid, s);
+    hipLaunchKernelGGL((xor_kernel_fixed<N, K, Args>), grid, dim3(kBlock), 0, s, a, g, sc);
     return launched("xor_kernel_fixed", grid, 0, s);
   }
   return hipErrorInvalidValue;
+}
+
+// Schedule of the straight-line XOR kernel: tiles per workgroup (skew K),
+// group order, write window. ECW_XOR_SCHED = "K,ORDER[,LOG2P,W]" overrides
+// the default (tuning; read per launch). K is 1 or ECW_XOR_SKEW_K (and 2, 4,
+// 8 in builds with -DECW_XOR_SKEW_ALL=1).
+#ifndef ECW_XOR_SKEW_K
+#define ECW_XOR_SKEW_K 4
+#endif
+#ifndef ECW_XOR_SKEW_ALL
+#define ECW_XOR_SKEW_ALL 0
+#endif
+struct XorChoice {
+  int skew;
+  uint32_t order, log2p, wwidth;
+};
+// Default: the diagonal skew for sources behind pointers (XorTab, XorPtr:
+// blocks the caller allocated, typically all at the same offset modulo 2 MiB
+// and beyond), the plain tile for slabs (their block strides carry a 4 KiB
+// stagger already). Interleaved in one process over the same blocks
+// (tools/repair_ab.py, profiles/r04_repair_ab_*.log), CL(128, 27, 3) D0
+// repair, 4 x 64 MiB stripes: separate torch allocations 6305 -> 6542 and
+// 6152 -> 6718 GB/s with K = 4 (tiled slab 6664 in the second process), one
+// allocation at block stride B 6072 -> 6733 and 5589 -> 6196; at stride
+// B + 4 KiB +0.4 %, split slab -1..-1.5 %. K = 2 / 8 and column-major group
+// order gain less.
+template <class Args>
+inline XorChoice xor_choice(const XorGeom&) {
+  constexpr bool ptrs = std::is_same<Args, XorTab>::value || std::is_same<Args, XorPtr>::value;
+  XorChoice c{ptrs ? ECW_XOR_SKEW_K : 1, 0, 11, 0};
+  if (const char* e = std::getenv("ECW_XOR_SCHED")) {
+    int k = 1;
+    unsigned o = 0, lp = 11, w = 0;
+    const int got = std::sscanf(e, "%d,%u,%u,%u", &k, &o, &lp, &w);
+    if (got >= 1) c.skew = k;
+    if (got >= 2) c.order = o ? 1 : 0;
+    if (got >= 4 && lp >= 4 && lp <= 24) {
+      c.log2p = lp;
+      c.wwidth = w;
+    }
+  }
+  return c;
+}
+
+template <int K, class Args>
+hipError_t launch_xor_skew(const Args& a, const XorGeom& g, const XorChoice& c, hipStream_t s) {
+  const uint64_t per = (g.tiles + K - 1) / K;
+  const uint64_t total = static_cast<uint64_t>(g.stripes) * per;
+  XorSched sc{};
+  sc.per = make_fastdiv(static_cast<uint32_t>(per));
+  sc.ns = make_fastdiv(static_cast<uint32_t>(g.stripes > 0 ? g.stripes : 1));
+  sc.order = c.order;
+  sc.wmask = (1u << c.log2p) - 1;
+  sc.wwidth = c.wwidth;
+  const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR));
+  return launch_xor_fixed<ECW_XOR_FIXED_MAX, K>(a, g, sc, grid, s);
 }
 
 template <class Args>
@@ -1030,7 +1136,16 @@ hipError_t launch_xor_range(const Args& a, const XorGeom& g, hipStream_t s) {
   // depth-8 ring over 1-2 sources would load every byte up to 8 times
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR)), block(kBlock);
   const FastDiv per = make_fastdiv(static_cast<uint32_t>(g.tiles));
-  if (g.n <= ECW_XOR_FIXED_MAX) return launch_xor_fixed<ECW_XOR_FIXED_MAX>(a, g, per, grid, s);
+  if (g.n <= ECW_XOR_FIXED_MAX) {
+    const XorChoice c = xor_choice<Args>(g);
+#if ECW_XOR_SKEW_ALL
+    if (c.skew == 2) return launch_xor_skew<2>(a, g, c, s);
+    if (c.skew == 8) return launch_xor_skew<8>(a, g, c, s);
+    if (c.skew == 4) return launch_xor_skew<4>(a, g, c, s);
+#endif
+    if (c.skew == ECW_XOR_SKEW_K) return launch_xor_skew<ECW_XOR_SKEW_K>(a, g, c, s);
+    return launch_xor_skew<1>(a, g, c, s);
+  }
   if (g.n <= 1)
     hipLaunchKernelGGL((xor_kernel<1, Args>), grid, block, 0, s, a, g, per);
   else if (g.n <= 2)
@@ -1360,7 +1475,9 @@ __global__ __launch_bounds__(kSvcThreads) void service_kernel(SvcCtl* ctl, SvcDe
     }
     const SvcReq& q = *req;  // read from LDS (a private copy would live in scratch)
     const int n16 = q.k * 8 * q.nw;
-    if (q.serial != staged || n16 != staged_n16) {
+    // a plain XOR (svc_request's XORROW path) reads no table: the staged ones stay
+    const bool xor_only = (q.flags & kSvcXorRow) && q.local_mode == kLocalNone && q.nw == 1;
+    if (!xor_only && (q.serial != staged || n16 != staged_n16)) {
       for (int i = threadIdx.x; i < n16; i += kSvcThreads) reinterpret_cast<uint4*>(lds)[i] = q.tbl[i];
       staged = q.serial;
       staged_n16 = n16;
@@ -1444,8 +1561,9 @@ hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, 
 }
 
 int stripes_per_launch(uint64_t tiles) {
-  const uint64_t n = kMaxTilesPerLaunch / (tiles ? tiles : 1);
-  return n > 0x7FFFFFFFull ? 0x7FFFFFFF : static_cast<int>(n);
+  // stripes * tiles < kMaxTilesPerLaunch, what the launchers' range checks accept
+  const uint64_t n = (kMaxTilesPerLaunch - 1) / (tiles ? tiles : 1);
+  return n > 0x7FFFFFFFull ? 0x7FFFFFFF : n < 1 ? 1 : static_cast<int>(n);  // (a 2^31-tile stripe: rejected by the range check)
 }
 
 int device_cu_count(int device) {

@@ -193,6 +193,18 @@ int ecw_encode_stripes(ecw_codec* codec, int stripes, const uint8_t* const* data
  * `out` receives the rebuilt `lost_block` (D or L). */
 int ecw_repair(ecw_codec* codec, const uint8_t* const* blocks, int lost_block, uint8_t* out, size_t len);
 
+/* Counters of the resident small-request service on `device` (host-memory
+ * calls of blocks up to 64 KiB: ecw_encode of one stripe, and the XORs of
+ * ecw_decode / ecw_partial_decode / ecw_repair / ecw_xor_intermediate), for
+ * callers that mix small and bulk calls (ECWide-H's proxy threads,
+ * ECWide-H/proxy/proxy.cpp:2001-2012) to see the service's hit rate:
+ * out[0] requests served, out[1] eligible requests that took the launch path
+ * instead (bulk work held the service off, or it was stopping), out[2]
+ * epochs launched, out[3] 1 if the service has turned itself off after a HIP
+ * error. No reference counterpart (observability). ECW_OK; zeros for a
+ * device the service never ran on. */
+int ecw_service_counters(int device, unsigned long long out[4]);
+
 /* ---- device-memory entry points (asynchronous on `stream`) -------------
  * All pointers are HBM addresses, 16-byte aligned. The pointer arrays
  * themselves are host arrays (copied into the kernel arguments). */

@@ -271,12 +271,12 @@ static void fastdiv() {
   CHECK(bad == 0);
   // launch ranges of the 32-bit tile numbering
   CHECK(ecw::stripes_per_launch(1) == 0x7FFFFFFF);
-  CHECK(ecw::stripes_per_launch(2) == (1 << 30));
-  CHECK(ecw::stripes_per_launch(16384) == (1 << 17));
+  CHECK(ecw::stripes_per_launch(2) == (1 << 30) - 1);
+  CHECK(ecw::stripes_per_launch(16384) == (1 << 17) - 1);
   CHECK(ecw::stripes_per_launch(1ull << 31) == 1);
   for (uint64_t t : {1ull, 2ull, 3ull, 4097ull, 1ull << 20})
-    CHECK(static_cast<uint64_t>(ecw::stripes_per_launch(t)) * t < (1ull << 31) + t &&
-          static_cast<uint64_t>(ecw::stripes_per_launch(t)) * t <= (1ull << 31));
+    CHECK(static_cast<uint64_t>(ecw::stripes_per_launch(t)) * t < (1ull << 31) &&
+          (static_cast<uint64_t>(ecw::stripes_per_launch(t)) + 1) * t >= (1ull << 31));
 }
 
 int main() {

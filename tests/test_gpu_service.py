@@ -269,3 +269,97 @@ def test_service_restages_tables_of_a_recreated_codec(E, orc):
                 assert np.array_equal(par[i], w), (it, i)
         finally:
             L.ecw_codec_destroy(h)
+
+
+def test_service_small_host_xors_vs_oracle(E, orc):
+    """decodeData / partialDecodeData / repairBlock / xorIntemediate on host
+    blocks up to 64 KiB are plain XORs served by the resident service (no
+    launch, no tables staged): bit-exact at ragged lengths, interleaved with
+    encodes of the same codec (whose tables the XOR requests leave staged in
+    LDS), and counted as served."""
+    k, m, r = 32, 2, 8
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, 65536), 1, False)
+    oc = orc.codec("C", k, m, r, 65536)
+    before = E.service_counters(c.device)
+    calls = 0
+    for n, ln in enumerate([4096, 1, 100, 5000, 3 * 1024 + 7, 65536]):
+        data = [orc.fill(ln, 400 + n, 0, j) for j in range(k)]
+        par = [np.full(ln, 0x5A, np.uint8) for _ in range(c.parityNum)]
+        c.encodeData(data, par)
+        want_par = orc.codec("C", k, m, r, ln).encode(data) if ln != 65536 else oc.encode(data)
+        assert all(np.array_equal(a, b) for a, b in zip(par, want_par)), (n, "encode")
+        ddn, pdn = c.decodeDataNum, c.partialDecodeNum
+        t = np.full(ln, 0x11, np.uint8)
+        c.decodeData(data[:ddn], t)
+        assert np.array_equal(t, orc.xor_blocks(data[:ddn])), (n, "decode")
+        t = np.full(ln, 0x22, np.uint8)
+        c.partialDecodeData(data[1:1 + pdn], t)
+        assert np.array_equal(t, orc.xor_blocks(data[1:1 + pdn])), (n, "partial")
+        blocks = data + par
+        out = np.zeros(ln, np.uint8)
+        c.repairBlock(blocks, 0, out)
+        assert np.array_equal(out, data[0]), (n, "repair")
+        tgt = [np.array(p) for p in par[:m]]
+        c.xorIntemediate(par[:m], tgt)
+        assert all(not t.any() for t in tgt), (n, "xorIntemediate")  # p ^ p
+        calls += 3 + m  # decode, partial decode, repair, m xorIntemediate XORs
+    after = E.service_counters(c.device)
+    assert not after["broken"]
+    assert after["served"] - before["served"] >= calls, (before, after)
+
+
+def test_service_not_stranded_by_bulk_holds(E, orc):
+    """bulk host calls (decodeData of 2 MiB blocks) hold the
+    service off while they run. A small request posted to an epoch that a
+    bulk call asked to leave must take the launch path at once, not spin
+    until every hold has ended (10 s, then the service was turned off for
+    good). Two threads keep holds overlapping back to back while a third makes
+    small encodes: every small call returns within 1 s, every byte is exact,
+    and once the bulk calls stop the service serves again."""
+    rs = E.NativeCodec.getRsCodec(E.CodingScheme.getRsScheme(11, 3, 4096))
+    ors = orc.codec("R", 11, 3, 11, 4096)
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(32, 2, 8, 2 << 20), 1, False)
+    ddn = c.decodeDataNum
+    stop = threading.Event()
+    errors, lat = [], []
+
+    def bulk(t):
+        data = [orc.fill(2 << 20, 600 + t, 0, j) for j in range(ddn)]
+        want = orc.xor_blocks(data)
+        out = np.zeros(2 << 20, np.uint8)
+        while not stop.is_set():
+            c.decodeData(data, out)
+            if not np.array_equal(out, want):
+                errors.append(("bulk", t))
+                return
+
+    def small():
+        data = [orc.fill(4096, 650, 0, j) for j in range(11)]
+        want = ors.encode(data)
+        par = [np.zeros(4096, np.uint8) for _ in range(3)]
+        while not stop.is_set():
+            t0 = time.perf_counter()
+            rs.encodeData(data, par)
+            lat.append(time.perf_counter() - t0)
+            if not all(np.array_equal(a, b) for a, b in zip(par, want)):
+                errors.append(("small",))
+                return
+
+    th = [threading.Thread(target=bulk, args=(t,)) for t in range(2)] + [threading.Thread(target=small)]
+    for x in th:
+        x.start()
+    time.sleep(3.0)
+    stop.set()
+    for x in th:
+        x.join()
+    assert not errors, errors[:5]
+    assert lat and max(lat) < 1.0, (len(lat), max(lat) if lat else None)
+    before = E.service_counters(rs.device)
+    data = [orc.fill(4096, 651, 0, j) for j in range(11)]
+    par = [np.zeros(4096, np.uint8) for _ in range(3)]
+    for _ in range(50):
+        rs.encodeData(data, par)
+    after = E.service_counters(rs.device)
+    print(f"\nsmall calls beside bulk holds: {len(lat)} calls, max {max(lat) * 1e3:.1f} ms; counters {after}")
+    assert not after["broken"]
+    assert after["served"] - before["served"] == 50, (before, after)
