@@ -64,6 +64,8 @@ def parse(argv=None):
     ap.add_argument("--other-layout-rounds", type=int, default=4, help="rounds of the interleaved layout legs")
     ap.add_argument("--configs4-steps", type=int, default=5,
                     help="timed steps of the configs[3]/[4] HBM-filling leg reported as `configs4` (0 = off)")
+    ap.add_argument("--shape-steps", type=int, default=5,
+                    help="timed steps of each other single-GPU BASELINE shape (configs1, configs0_shape; 0 = off)")
     ap.add_argument("--host-iters", type=int, default=2,
                     help="rank 0: encodes + repairs of the PCIe-inclusive host-resident leg (0 = off)")
     ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
@@ -157,6 +159,11 @@ class Dist:
             # the same on one GPU or eight, and no RCCL communicator is set up
             dist.init_process_group("gloo")
             self.backend = dist.get_backend()
+            if not self.dry:
+                # one process per GPU: with enough GPUs every rank must sit on its own
+                devs = self.gather(float(torch.cuda.current_device()))
+                if self.distinct and len(set(devs)) != self.world:
+                    raise SystemExit(f"bench.py: ranks share GPUs {devs} although {self.ndev} are visible")
 
     def _tensor(self, vals):
         import torch
@@ -317,6 +324,10 @@ def cpu_baseline(args, k, m, r, B):
 
     res = {}
     allc = host_threads()
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
     run(allc)  # warm: fault in the output pages outside the timing
     for threads in sorted({1, allc}):
         n, t0 = 0, time.perf_counter()
@@ -337,7 +348,11 @@ def cpu_baseline(args, k, m, r, B):
                    f"flow (AVX2 nibble-pshufb port of ISA-L's gf_Nvect_dot_prod_avx2, global + per-group passes) "
                    f"+ decodeData of D0; 1 thread = ECWide-C's one ComputeWorker thread"),
         "value_all_cores": round(res[allc], 3),
-        "cores_all": allc,
+        "cores_all": allc,  # threads the all-cores run used: min(affinity_cores, OMP_NUM_THREADS, cap)
+        "affinity_cores": affinity,
+        "nproc": os.cpu_count(),
+        "cap": 16,  # host_threads(): the GPU box's per-GPU CPU share (OMP_NUM_THREADS=16 there)
+        "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
         "host_cpu": host_cpu_model(),
         "avx2": orc.have_avx2(),
     }
@@ -377,13 +392,16 @@ def verify(args, slab, out, pl, k, m, r) -> dict:
         res["repairs"] += 1
     mf = os.path.join(REPO, "tests", "golden", "manifest.json")
     if s0 == 0 and off0 == 0 and os.path.exists(mf):
-        e = next((x for x in json.load(open(mf)).get("full", []) if x["name"] == "cfg3_full"), None)
-        if e and (e["k"], e["m"], e["r"], e["len"], e["seed"]) == (k, m, r, B, args.seed):
+        # the full-size digests of this shape and seed (cfg1_full / cfg2_full / cfg3_full), if committed
+        e = next((x for x in json.load(open(mf)).get("full", [])
+                  if (x["k"], x["m"], x["r"], x["len"], x["seed"]) == (k, m, r, B, args.seed)), None)
+        if e:
             got = [hashlib.sha256(p.cpu().numpy().tobytes()).hexdigest() for p in slab.parity(0)]
             rep = hashlib.sha256(out[:B].cpu().numpy().tobytes()).hexdigest()
             if got != e["parity_sha256"] or rep != e["repair_d0_sha256"]:
-                return dict(res, ok=False, failed="stripe 0 vs manifest cfg3_full digests")
+                return dict(res, ok=False, failed=f"stripe 0 vs manifest {e['name']} digests")
             res["digests"] = True
+            res["digest_entry"] = e["name"]
     return dict(res, ok=True)
 
 
@@ -744,18 +762,33 @@ def dry_run(args, d: Dist):
     el_max = d.reduce(el, "max")
     shares = [d.gather(float(sh[key])) for key in ("s0", "stripes", "block_bytes", "col_offset")]
     per_rank = d.gather(el)
+    steps = max(1, args.steps)
     c4 = None
     if args.configs4_steps > 0 and not args.hbm_fill:
         p4 = plan(args, d, free, m + g, fill=True)
         c4 = {"stripes_total": p4["stripes_total"], "block_bytes": p4["block_bytes_full"],
+              "stripes_per_gpu": p4["share"]["stripes"],
+              "rank_ms_per_step": [round(x / args.configs4_steps * 1e3, 4) for x in d.gather(el)],
               "shares": [dict(s0=int(a), stripes=int(b)) for a, b in
                          zip(*[d.gather(float(p4["share"][key])) for key in ("s0", "stripes")])]}
+    shapes = {}
+    if args.shape_steps > 0 and not args.hbm_fill and not args.strong:
+        for name, _, sk, sm, sr, mib, stripes, seed in SHAPE_LEGS:
+            a = argparse.Namespace(**vars(args))
+            a.k, a.m, a.r, a.block_mib, a.stripes, a.seed, a.strong = sk, sm, sr, float(mib), stripes, seed, False
+            ps = plan(a, d, free, sm + -(-sk // sr))
+            shapes[name] = {"stripes_per_gpu": ps["share"]["stripes"], "stripes_total": ps["stripes_total"],
+                            "block_bytes": ps["block_bytes_full"],
+                            "rank_ms_per_step": [round(x / args.shape_steps * 1e3, 4) for x in d.gather(el)]}
+    d.barrier()  # the rank-0-only host legs start after every rank's timed legs
     if d.rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": d.world, "scaling": "strong" if pl["strong"] else "weak",
                           "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
                           "block_bytes": pl["block_bytes_full"], "el_max": el_max, "rank_seconds": per_rank,
+                          "rank_ms_per_step": [round(x / steps * 1e3, 4) for x in per_rank],
+                          "roofline": {"rank_launch_ms": [round(x * 1e3 / steps, 4) for x in per_rank]},
                           "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
-                          "configs4": c4,
+                          "configs4": c4, **shapes,
                           "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
                                      for a, b, c, o in zip(*shares)]}), flush=True)
     d.close()
@@ -813,7 +846,7 @@ def device_leg(args, d: Dist, E, pl: dict, k: int, m: int, r: int, steps: int, w
     enc_ms = sum(e[0].elapsed_time(e[1]) for e in evs) / steps
     rep_ms = sum(e[1].elapsed_time(e[2]) for e in evs) / steps
     return dict(codec=codec, slab=slab, out=out, enc_bytes=enc_bytes, rep_bytes=rep_bytes, el_max=el_max,
-                rank_s=rank_s, enc_ms=enc_ms, rep_ms=rep_ms,
+                rank_s=rank_s, enc_ms=enc_ms, rep_ms=rep_ms, rank_enc_ms=d.gather(enc_ms),
                 enc_ms_max=d.reduce(enc_ms, "max"), rep_ms_max=d.reduce(rep_ms, "max"))
 
 
@@ -822,14 +855,18 @@ def pmc_traffic(args, k, r, m, B, S, enc_bytes, launches):
     written by tools/prof_summary.py from separate FETCH_SIZE / WRITE_SIZE
     rocprofv3 passes over this very workload), or None."""
     if not os.path.exists(args.pmc):
-        return None
+        return None, None
     try:
         pmc = json.load(open(args.pmc))
         key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{args.chunk_kib}k", "split": "_split"}.get(args.layout, "")
         ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
-        return ratio * enc_bytes / launches if ratio else None
+        if not ratio:
+            return None, None
+        src = (f"profiles/{os.path.basename(args.pmc)}[{key}]: traffic/algorithmic ratio of separate rocprofv3 "
+               f"FETCH_SIZE / WRITE_SIZE passes over this workload (committed; not measured in this run)")
+        return ratio * enc_bytes / launches, src
     except Exception:
-        return None
+        return None, None
 
 
 def configs4_leg(args, d: Dist, E, k, m, r) -> dict:
@@ -861,6 +898,57 @@ def configs4_leg(args, d: Dist, E, k, m, r) -> dict:
         "encode_launch_ms": round(leg["enc_ms_max"] / launches, 4), "launches_per_encode": launches,
         "verified": bool(ok),
         "verify": {key: vres[key] for key in ("windows", "repairs")} | ({"failed": vres["failed"]} if not vres["ok"] else {}),
+    }
+    del leg
+    torch.cuda.empty_cache()
+    return res
+
+
+# The other single-GPU BASELINE shapes, each its own timed leg of the line (weak:
+# the stripes are per GPU), stripe 0 pinned by the committed full-size digests
+# of the same shape and seed (tests/golden/manifest.json).
+SHAPE_LEGS = [
+    # name, BASELINE config, k, m, r, block MiB, stripes per GPU, seed (= manifest entry)
+    ("configs1", "configs[1]: (k=32, 4 local groups, 2 global parities), 16 MiB/block", 32, 2, 8, 16, 32, 102),
+    ("configs0_shape", "configs[0]'s default ECWide-C/config/scheme.ini shape (CL k=32, groupDataNum=11, "
+                      "globalParityNum=3, chunkSizeBits=26) on the device", 32, 3, 11, 64, 8, 101),
+]
+
+
+def shape_leg(args, d: Dist, E, leg_def) -> dict:
+    """One SHAPE_LEGS entry: fill, time `--shape-steps` steps (encode of the
+    slab + repair of D0 of every stripe) exactly as the main leg, verify
+    (oracle windows, every repair, stripe 0 vs the digests)."""
+    import torch
+
+    name, desc, k, m, r, mib, stripes, seed = leg_def
+    a = argparse.Namespace(**vars(args))
+    a.k, a.m, a.r, a.block_mib, a.stripes, a.seed, a.strong = k, m, r, float(mib), stripes, seed, False
+    g = -(-k // r)
+    torch.cuda.empty_cache()
+    pl = plan(a, d, 0, m + g)
+    leg = device_leg(a, d, E, pl, k, m, r, args.shape_steps, 2, args.layout)
+    vres = verify(a, leg["slab"], leg["out"], pl, k, m, r)
+    ok = d.reduce(1.0 if vres["ok"] else 0.0, "min") > 0.5
+    sh = pl["share"]
+    total_bytes = (leg["enc_bytes"] + leg["rep_bytes"]) * pl["stripes_total"] // sh["stripes"] * args.shape_steps
+    launches = leg["slab"].encode_launches()
+    enc = leg["enc_bytes"] / (leg["enc_ms_max"] * 1e-3) / 1e9
+    rep = leg["rep_bytes"] / (leg["rep_ms_max"] * 1e-3) / 1e9
+    res = {
+        "baseline_config": desc,
+        "workload": workload_of(pl, k, m, r, g, d.world) + f", seed {seed}",
+        "value": round(total_bytes / leg["el_max"] / 1e9, 2), "unit": "GB/s",
+        "ms_per_step": round(leg["el_max"] / args.shape_steps * 1e3, 4), "steps": args.shape_steps,
+        "scaling": "weak", "stripes_per_gpu": sh["stripes"], "block_bytes": pl["block_bytes_full"],
+        "rank_ms_per_step": [round(x / args.shape_steps * 1e3, 4) for x in leg["rank_s"]],
+        "encode_GBps": round(enc, 2), "repair_GBps": round(rep, 2),
+        "encode_frac": round(enc / HBM_PEAK_GBS, 4), "repair_frac": round(rep / HBM_PEAK_GBS, 4),
+        "encode_launch_ms": round(leg["enc_ms_max"] / launches, 4), "launches_per_encode": launches,
+        "verified": bool(ok),
+        "verify": {key: vres[key] for key in ("windows", "repairs", "digests")}
+        | ({"digest_entry": vres["digest_entry"]} if "digest_entry" in vres else {})
+        | ({"failed": vres["failed"]} if not vres["ok"] else {}),
     }
     del leg
     torch.cuda.empty_cache()
@@ -909,7 +997,7 @@ def main():
     # the slowest rank's kernel times: a per-GPU roofline that holds for every GPU
     enc_ms, rep_ms = leg["enc_ms_max"], leg["rep_ms_max"]
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(args, k, r, m, B, S, enc_bytes, launches)
+    traffic, traffic_src = pmc_traffic(args, k, r, m, B, S, enc_bytes, launches)
     line = {
         "metric": "device-resident encode + single-block-repair GB/s, wide stripe (shards in HBM)",
         "value": round(value, 2),
@@ -936,11 +1024,14 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "per_gpu": "the slowest rank's launch time" if d.world > 1 else "one GPU",
             # PMC-measured HBM bytes of one launch over this run's launch time
             "traffic_GBps": round(traffic * launches / (enc_ms * 1e-3) / 1e9, 2) if traffic else None,
             # per kernel launch (rocprof's unit); one encode() of the slab = `launches` launches
             "launch_ms": round(enc_ms / launches, 4),
+            # every rank's own encode launch time (a slow GPU shows here; launch_ms is their max)
+            "rank_launch_ms": [round(x / launches, 4) for x in leg["rank_enc_ms"]],
             "algorithmic_bytes_per_launch": enc_bytes // launches,
             "launches_per_encode": launches,
             "encode_call_ms": round(enc_ms, 4),
@@ -959,6 +1050,10 @@ def main():
     torch.cuda.empty_cache()
     if args.configs4_steps > 0 and not pl["hbm_fill"]:
         line["configs4"] = configs4_leg(args, d, E, k, m, r)
+    if args.shape_steps > 0 and not pl["hbm_fill"] and not args.strong:
+        for leg_def in SHAPE_LEGS:
+            line[leg_def[0]] = shape_leg(args, d, E, leg_def)
+    d.barrier()  # the rank-0-only host legs below never overlap another rank's timed region
     if d.rank == 0:
         if args.cpu_seconds > 0:
             line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)

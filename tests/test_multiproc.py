@@ -200,6 +200,23 @@ def test_bench_config_same_at_every_n():
         assert c4["stripes_total"] == 256 and sum(x["stripes"] for x in c4["shares"]) == 256
 
 
+def test_bench_dry_run_n8_per_rank_fields():
+    """the driver's first 8-GPU run. Every per-rank field
+    has 8 entries, the configs[4] split gives each GPU 32 of the 256 stripes,
+    and the k=32 shape legs keep their per-GPU stripe counts (weak)."""
+    p, line = _bench("--gpus", "8", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    assert line["n_gpus"] == 8 and len(line["rank_ms_per_step"]) == 8
+    assert len(line["roofline"]["rank_launch_ms"]) == 8
+    c4 = line["configs4"]
+    assert c4["stripes_per_gpu"] == 32 and len(c4["rank_ms_per_step"]) == 8
+    assert [x["stripes"] for x in c4["shares"]] == [32] * 8
+    assert line["configs1"]["stripes_per_gpu"] == 32 and line["configs1"]["stripes_total"] == 256
+    assert line["configs1"]["block_bytes"] == 16 << 20
+    assert line["configs0_shape"]["stripes_per_gpu"] == 8 and line["configs0_shape"]["block_bytes"] == 64 << 20
+    assert len(line["configs0_shape"]["rank_ms_per_step"]) == 8
+
+
 def test_bench_dry_run_strong_and_column_modes():
     p, line = _bench("--gpus", "2", "--dry-run", "--strong", "--stripes", "6")
     assert p.returncode == 0, p.stderr[-2000:]

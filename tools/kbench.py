@@ -95,8 +95,8 @@ def main():
                             dtype=torch.int64, device="cuda")
         buf = blocks[0]
         idx = (ctypes.c_int * 256)()
-        nsrc = L0.ecw_repair_sources(libs[0][2], 0, idx, 256)
-        assert nsrc > 0
+        # RS codes have no local groups: no repair sources, the repair leg is skipped
+        nsrc = L0.ecw_repair_sources(libs[0][2], 0, idx, 256) if a.code == "C" else 0
         stab = torch.tensor([blocks[s_ * nblk + idx[i]].data_ptr() for s_ in range(S) for i in range(nsrc)],
                             dtype=torch.int64, device="cuda")
         outs = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(S)]
@@ -139,7 +139,7 @@ def main():
                     st = L.ecw_encode_batch_dev(h, c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream)
                     assert st == 0, (name, st)
             e[1].record()
-            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split else 0  # literal L: no repair
+            rep_iters = a.iters if a.code == "C" and not a.literal and not a.split and not (a.tables and nsrc <= 0) else 0  # literal L: no repair
             for it in range(rep_iters):
                 if a.tables:
                     st = L.ecw_xor_reduce_ptrs_dev(0, S, nsrc, c_void_p(stab.data_ptr()), c_void_p(otab.data_ptr()),
