@@ -7,6 +7,7 @@ interleaved rounds (placement differs per allocation).
 Placements (S stripes of CL(k, r, m), B-byte blocks):
   tiled     StripeSlab tiled layout (8 KiB pieces; the bench's headline layout)
   split     whole blocks at stride B + 4 KiB, parity blocks in a region of their own
+  blocks    whole blocks at stride B + 4 KiB, [D.., G.., L..] per stripe (the block slab)
   sep       every block its own torch.empty(B) (the bench's pointer leg)
   carved0   pointer tables into one allocation, block stride exactly B
   carved4k  the same at block stride B + 4 KiB
@@ -89,20 +90,33 @@ def main():
                 pbuf = torch.empty(units * np_ * ch, dtype=torch.uint8, device="cuda")
                 args = (c_void_p(dbuf.data_ptr()), ch, k * ch, c_void_p(pbuf.data_ptr()), ch, np_ * ch)
                 n_units, ulen = units, ch
-                d0 = [(lambda s=s: dbuf.view(S, B // ch, k, ch)[s, :, 0, :].reshape(-1)) for s in range(S)]
+                d0 = [(lambda s=s, buf=dbuf, ch=ch: buf.view(S, B // ch, k, ch)[s, :, 0, :].reshape(-1)) for s in range(S)]
             else:
                 bs = B + 4096
                 dbuf = torch.empty(S * k * bs, dtype=torch.uint8, device="cuda")
                 pbuf = torch.empty(S * np_ * bs, dtype=torch.uint8, device="cuda")
                 args = (c_void_p(dbuf.data_ptr()), bs, k * bs, c_void_p(pbuf.data_ptr()), bs, np_ * bs)
                 n_units, ulen = S, B
-                d0 = [(lambda s=s: dbuf[s * k * bs:s * k * bs + B]) for s in range(S)]
+                d0 = [(lambda s=s, buf=dbuf, bs=bs: buf[s * k * bs:s * k * bs + B]) for s in range(S)]
             dbuf.random_(0, 256, generator=gen)
             keep.append((dbuf, pbuf))
             enc = (lambda args=args, n=n_units, ln=ulen:
                    L.ecw_encode_batch_split_dev(h, *args, n, ln, stream))
             rep = (lambda args=args, n=n_units, ln=ulen:
                    L.ecw_repair_batch_split_dev(h, *args, n, 0, c_void_p(out.data_ptr()), ln, ln, stream))
+            legs[p] = (enc, rep, d0)
+            continue
+        if p == "blocks":  # the block slab: [D.., G.., L..] per stripe at block stride B + 4 KiB
+            bs = B + 4096
+            big = torch.empty(S * (k + np_) * bs, dtype=torch.uint8, device="cuda")
+            big.random_(0, 256, generator=gen)
+            keep.append(big)
+            enc = (lambda big=big, bs=bs:
+                   L.ecw_encode_batch_dev(h, c_void_p(big.data_ptr()), bs, (k + np_) * bs, S, B, stream))
+            rep = (lambda big=big, bs=bs:
+                   L.ecw_repair_batch_dev(h, c_void_p(big.data_ptr()), bs, (k + np_) * bs, S, 0,
+                                          c_void_p(out.data_ptr()), B, B, stream))
+            d0 = [(lambda s=s, big=big, bs=bs: big[s * (k + np_) * bs:][:B]) for s in range(S)]
             legs[p] = (enc, rep, d0)
             continue
         if p == "sep":
@@ -133,7 +147,7 @@ def main():
     rep_bytes = S * (nsrc + 1) * B
     enc_bytes = S * (k + np_) * B
     res, encw = {}, {}
-    combos = [(p, sc) for p in legs for sc in (a.scheds if p not in ("tiled",) else a.scheds[:1])]
+    combos = [(p, sc) for p in legs for sc in a.scheds]
     for rd in range(a.rounds):
         order = combos[rd % len(combos):] + combos[:rd % len(combos)]
         for p, sc in order:
