@@ -721,17 +721,39 @@ def ecwide_h_sequence(args, shim, orc, ln: int) -> dict:
     verified = all(np.array_equal(x, y) for og, oc in zip(bg[1], bc[1]) for x, y in zip(og, oc))
     n = max(1000, args.small_calls_n // 2)
 
-    def timed(fn, nt):
+    def timed(fn, nt, service=False):
+        import numpy as np
+
+        import ecwide_amd as E
+
         bs = [bufs() for _ in range(nt)]
-        th = [threading.Thread(target=lambda b=b: [fn(b) for _ in range(n)]) for b in bs]
+        lat = [[] for _ in range(nt)]
+
+        def work(i):
+            for _ in range(n):
+                t = time.perf_counter()
+                fn(bs[i])
+                lat[i].append(time.perf_counter() - t)
+
+        th = [threading.Thread(target=work, args=(i,)) for i in range(nt)]
+        c0 = E.service_counters(0) if service else None
         t0 = time.perf_counter()
         for x in th:
             x.start()
         for x in th:
             x.join()
         el = time.perf_counter() - t0
-        return {"threads": nt, "sequences": n * nt, "us_per_sequence_per_thread": round(el / n * 1e6, 2),
-                "GBps": round(n * nt * nbytes / el / 1e9, 3)}
+        res = {"threads": nt, "sequences": n * nt, "us_per_sequence_per_thread": round(el / n * 1e6, 2),
+               "GBps": round(n * nt * nbytes / el / 1e9, 3)}
+        all_lat = np.array([x for row in lat for x in row]) * 1e6
+        res["us_per_sequence_p50_p99"] = [round(float(np.percentile(all_lat, q)), 2) for q in (50, 99)]
+        if service:
+            # every call of a sequence is a service candidate (<= 64 KiB, <= 8 rows)
+            c1 = E.service_counters(0)
+            served, declined = c1["served"] - c0["served"], c1["declined"] - c0["declined"]
+            res["service"] = {"served": served, "declined": declined,
+                              "hit_rate": round(served / max(1, served + declined), 4), "broken": c1["broken"]}
+        return res
 
     # one thread each: driven from Python, the 16 ctypes calls of a sequence
     # cost both sides the same interpreter time, and more threads would only
@@ -739,7 +761,7 @@ def ecwide_h_sequence(args, shim, orc, ln: int) -> dict:
     return {"calls": "l_encode 11->1 XOR, g_encode 11->3 Cauchy, l_middle 4->1 XOR, l_decode 5->1 XOR, "
                      "tables rebuilt per call; driven from Python on both sides",
             "bytes_per_sequence": nbytes, "verified": bool(verified),
-            "gpu": timed(gpu_run, 1), "cpu_port": timed(cpu_run, 1)}
+            "gpu": timed(gpu_run, 1, service=True), "cpu_port": timed(cpu_run, 1)}
 
 
 # ---- the bench ------------------------------------------------------------------

@@ -508,6 +508,59 @@ def test_xor_reduce_ptrs_dev_vs_oracle(E, torch, orc, n, ln, S):
         assert (got[ln:] == 0x5A).all(), s
 
 
+@pytest.mark.parametrize("sched", [None, "1,0", "4,0", "4,1", "1,1", "4,0,11,64", "1,0,10,32", "4,1,12,128"])
+def test_xor_schedules_same_bytes(E, torch, orc, monkeypatch, sched):
+    """Every XOR schedule (ecw_kernels.hip launch_xor_range; ECW_XOR_SCHED =
+    "K,ORDER[,LOG2P,W]": K column tiles per workgroup read diagonally,
+    column-major group order, write window; None = the library's choice) gives
+    the oracle's bytes through all four source forms (pointer mode, device
+    pointer tables, split slab, block slab), with whole groups of K tiles, a
+    ragged last group and a ragged last tile, at several fan-ins, and writes
+    nothing past a block."""
+    from ctypes import c_void_p
+
+    from ecwide_amd._lib import lib
+
+    if sched is None:
+        monkeypatch.delenv("ECW_XOR_SCHED", raising=False)
+    else:
+        monkeypatch.setenv("ECW_XOR_SCHED", sched)
+    ln, S = 5 * 16384 + 2 * 4096 + 48, 3
+    strm = c_void_p(torch.cuda.current_stream().cuda_stream)
+    for n in (1, 5, 27, 32):
+        data = [[orc.fill(ln, 500 + n, s, i) for i in range(n)] for s in range(S)]
+        want = [orc.xor_blocks(row) for row in data]
+        src = [[torch.from_numpy(d).cuda() for d in row] for row in data]
+        # pointer mode (XorPtr)
+        out = torch.full((ln + 32,), 0xA5, dtype=torch.uint8, device="cuda")
+        E.xor_reduce(src[0], out[:ln])
+        torch.cuda.synchronize()
+        assert np.array_equal(out[:ln].cpu().numpy(), want[0]) and (out[ln:].cpu().numpy() == 0xA5).all(), n
+        # device pointer tables (XorTab)
+        dst = [torch.full((ln + 32,), 0x5A, dtype=torch.uint8, device="cuda") for _ in range(S)]
+        st = torch.tensor([b.data_ptr() for row in src for b in row], dtype=torch.int64, device="cuda")
+        dt = torch.tensor([d.data_ptr() for d in dst], dtype=torch.int64, device="cuda")
+        assert lib.ecw_xor_reduce_ptrs_dev(0, S, n, c_void_p(st.data_ptr()), c_void_p(dt.data_ptr()), ln, strm) == 0
+        torch.cuda.synchronize()
+        for s in range(S):
+            got = dst[s].cpu().numpy()
+            assert np.array_equal(got[:ln], want[s]) and (got[ln:] == 0x5A).all(), (n, s)
+    # slabs (XorSplit, XorSlab): CL repair of D0 from its group
+    k, r = 40, 27
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, 2, r, ln), 1, False)
+    for layout in ("split", "blocks"):
+        slab = E.StripeSlab(c, stripes=S, block_bytes=ln, layout=layout)
+        slab.fill_random(seed=91)
+        slab.encode()
+        out = torch.full((S * slab.out_stride,), 0x33, dtype=torch.uint8, device="cuda")
+        for lost in (0, k + 2):
+            slab.repair(lost, out)
+            torch.cuda.synchronize()
+            for s in range(S):
+                assert torch.equal(out[s * slab.out_stride:s * slab.out_stride + ln], slab.block(s, lost)), \
+                    (layout, lost, s)
+
+
 def test_block_batch_encode_repair(E, torch, orc):
     """BlockBatch: a batch of stripes of separately allocated blocks, encoded and
     every D and L block repaired through device pointer tables, one launch each."""
