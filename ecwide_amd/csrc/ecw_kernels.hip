@@ -955,11 +955,12 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 inline bool window_shape(const EncodeGeom& g) {
   return g.k >= 64 && g.nrows <= 4 && g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
 }
-// slabs: only with the parity rows in the slab after each stripe's data rows
-inline bool window_auto(const SlabRows& r, const EncodeGeom& g) {
-  return window_shape(g) && r.pbstride == r.bstride && r.psstride == r.sstride &&
-         r.pbase == r.base + static_cast<uint64_t>(g.k) * r.bstride;
-}
+// Slabs of whole blocks: the block slab (parity rows after each stripe's data
+// rows) since round 2; the split slab (parities in a region of their own)
+// since round 4, interleaved in one process: 5557 -> 6350 and 5846 -> 6285 GB/s
+// (profiles/r04b_repair_ab_*.log; round 2 had measured +5.0 / -2.4 % on two
+// boxes). The tiled slab's 8 KiB units are below window_shape's 64 KiB.
+inline bool window_auto(const SlabRows&, const EncodeGeom& g) { return window_shape(g); }
 inline bool window_auto(const PtrRows&, const EncodeGeom& g) { return window_shape(g); }
 inline bool window_auto(const PtrTabRows&, const EncodeGeom& g) { return window_shape(g); }
 
@@ -1085,25 +1086,39 @@ struct XorChoice {
   int skew;
   uint32_t order, log2p, wwidth;
 };
-// Default: the diagonal skew for sources behind pointers (XorTab, XorPtr:
-// blocks the caller allocated, typically all at the same offset modulo 2 MiB
-// and beyond), the plain tile for slabs (their block strides carry a 4 KiB
-// stagger already). Interleaved in one process over the same blocks
-// (tools/repair_ab.py, profiles/r04_repair_ab_*.log), CL(128, 27, 3) D0
-// repair, 4 x 64 MiB stripes: separate torch allocations 6305 -> 6542 and
-// 6152 -> 6718 GB/s with K = 4 (tiled slab 6664 in the second process), one
-// allocation at block stride B 6072 -> 6733 and 5589 -> 6196; at stride
-// B + 4 KiB +0.4 %, split slab -1..-1.5 %. K = 2 / 8 and column-major group
-// order gain less.
+// Default, from interleaved A/Bs in one process over the same blocks
+// (tools/repair_ab.py; profiles/r04_repair_ab_*.log, r04b_*, r04c_*; CL D0
+// repair, 4 stripes of 64 MiB blocks):
+//  * whole blocks (>= 64 KiB: the reference's per-block buffers, the split
+//    and block slabs) take the diagonal skew, K = 4: blocks allocated one by
+//    one start at the same offset modulo 2 MiB and beyond, so one column of
+//    all n sources can sit on one HBM channel and bank a row apart; reading
+//    the sources at K different column tiles at once spreads them. Separate
+//    torch allocations 6008 -> 6248, one allocation at block stride B 5973 ->
+//    6423 GB/s at n = 27; n = 4: 5950 -> 6540;
+//  * ... and, from n >= 8 sources and 8192 column tiles per launch, the write
+//    window (2^11 ticks, W = 64, as the encode's): n = 27 separate blocks 6612,
+//    stride-B allocation 6734, split slab 5847 -> 6658 in a process where it
+//    had landed slowly (+0.6 % where it had not), block slab 6658 -> 6765;
+//    n = 9 6550-6558 against 6191-6320 without it. Below 8 sources a tile's
+//    reads take too few window periods and the window locks the workgroups
+//    into generations (n = 4: -2..-10 %; K = 1 with the window: -50..-70 %);
+//  * the tiled slab's 8 KiB units keep K = 1 and no window (K = 4: -0.5..-8 %,
+//    window -2..-70 %: its sources are one contiguous run already).
+// Column-major group order and K = 2 / 8 gained less than K = 4 everywhere.
 template <class Args>
-inline XorChoice xor_choice(const XorGeom&) {
-  constexpr bool ptrs = std::is_same<Args, XorTab>::value || std::is_same<Args, XorPtr>::value;
-  XorChoice c{ptrs ? ECW_XOR_SKEW_K : 1, 0, 11, 0};
+inline XorChoice xor_choice(const XorGeom& g) {
+  const bool whole = g.len >= 65536;
+  XorChoice c{whole ? ECW_XOR_SKEW_K : 1, 0, 11, 0};
+  if (whole && g.n >= 8 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192) c.wwidth = 64;
   if (const char* e = std::getenv("ECW_XOR_SCHED")) {
     int k = 1;
     unsigned o = 0, lp = 11, w = 0;
     const int got = std::sscanf(e, "%d,%u,%u,%u", &k, &o, &lp, &w);
-    if (got >= 1) c.skew = k;
+    if (got >= 1) {  // an override names the whole schedule: no window unless given
+      c.skew = k;
+      c.wwidth = 0;
+    }
     if (got >= 2) c.order = o ? 1 : 0;
     if (got >= 4 && lp >= 4 && lp <= 24) {
       c.log2p = lp;

@@ -349,7 +349,7 @@ def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, lay
     """The write window (ecw_kernels.hip set_write_window) only delays the
     parity stores: encodes with it forced off, on, and at another period give
     identical parities, equal to the oracle on a column window, and the default
-    choice ('auto': block slab and pointer modes at k >= 64, <= 4 global rows, whole blocks >= 64 KiB,
+    choice ('auto': whole-block slabs and pointer modes at k >= 64, <= 4 global rows, blocks >= 64 KiB,
     >= 8192 tiles) is one of them."""
     B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
