@@ -13,3 +13,8 @@ timeout -k 10 300 python -u tools/layout_ab.py --k 32 --m 3 --r 11 --mib 64 --st
 timeout -k 10 300 python -u tools/layout_ab.py --k 128 --m 3 --r 27 --mib 64 --stripes 8 --rounds 3 \
   --variants tiled:8192:0,tiled:16384:0,tiled:4096:0 > gpurun_out/r04_k128_piece.log 2>&1
 timeout -k 10 400 python -u tools/cpu_baseline.py > gpurun_out/r04_cpu_baselines.log 2>&1
+# tiled slab repair: K = 2 (both 4 KiB tiles of an 8 KiB unit in one workgroup), column-major order
+timeout -k 10 300 python -u tools/repair_ab.py --lib build/variants/skewall.so --stripes 8 --rounds 4 \
+  --placements tiled --scheds 1,0 2,0 1,1 2,1 > gpurun_out/r04_tiled_repair_k2.log 2>&1
+timeout -k 10 300 python -u tools/repair_ab.py --lib build/variants/skewall.so --stripes 32 --rounds 4 --k 32 --m 2 \
+  --r 8 --mib 16 --placements tiled --scheds 1,0 2,0 1,1 2,1 > gpurun_out/r04_tiled_repair_k2_cfg1.log 2>&1

@@ -22,6 +22,9 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 
 LEGS = [("sep", "1,0"), ("sep", "4,0"), ("sep", "auto"), ("split", "1,0"), ("split", "4,0"), ("split", "auto")]
+# then the encode of each placement (write window: the library's choice), `reps` encodes of 2 launches each
+ENC_LEGS = ["sep", "split", "tiled"]
+ENC_LAUNCHES = 2
 
 
 def run(a):
@@ -63,20 +66,38 @@ def run(a):
               f"{S * (r + 1) * B / (ms * 1e-3) / 1e9:.1f} GB/s", flush=True)
     ok = torch.equal(outs[0], data[0][0]) and torch.equal(out[:B], split.block(0, 0))
     print(f"repairs == D0: {ok}")
+    os.environ.pop("ECW_XOR_SCHED", None)
+    tiled = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled")
+    tiled.fill_random(seed=5)
+    assert tiled.encode_launches() == ENC_LAUNCHES and split.encode_launches() == ENC_LAUNCHES
+    enc = {"sep": batch.encode, "split": split.encode, "tiled": tiled.encode}
+    for place in ENC_LEGS:
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+        e[0].record()
+        for _ in range(a.reps):
+            enc[place]()
+        e[1].record()
+        torch.cuda.synchronize()
+        ms = e[0].elapsed_time(e[1]) / a.reps
+        print(f"{place:6s} encode {a.reps} x {ENC_LAUNCHES} dispatches, {ms:.4f} ms per encode, "
+              f"{S * (k + np_) * B / (ms * 1e-3) / 1e9:.1f} GB/s", flush=True)
 
 
 def summarize(a):
     per = defaultdict(lambda: defaultdict(float))  # dispatch id -> counter -> value
+    eper = defaultdict(lambda: defaultdict(float))
     names = {}
     for path in a.summarize:
         with open(path) as f:
             for row in csv.DictReader(f):
                 name = row.get("Kernel_Name", "")
-                if "xor_kernel_fixed" not in name:
+                tgt = per if "xor_kernel_fixed" in name else eper if "encode_kernel_asm" in name else None
+                if tgt is None:
                     continue
                 d = int(row["Dispatch_Id"])
-                per[d][row["Counter_Name"]] += float(row["Counter_Value"])
+                tgt[d][row["Counter_Name"]] += float(row["Counter_Value"])
                 names[d] = name
+    summarize_encode(a, eper)
     ids = sorted(per)
     if len(ids) != len(LEGS) * a.reps:
         print(f"warning: {len(ids)} xor dispatches, expected {len(LEGS) * a.reps}")
@@ -98,6 +119,28 @@ def summarize(a):
         kern = names[grp[0]].split("(")[0][-60:]
         print(f"{place:6s} sched {sched:5s} [{kern}] " + " ".join(f"{c}={v:.4g}" for c, v in avg.items()) + extra
               + f" (algorithmic {alg / 1e9:.3f} GB/dispatch)")
+
+
+def summarize_encode(a, eper):
+    ids = sorted(eper)
+    n = a.reps * ENC_LAUNCHES
+    # the encodes before the timed legs (one per placement) come first: take the last len(ENC_LEGS) * n
+    ids = ids[-len(ENC_LEGS) * n:]
+    B, S, k, np_ = 64 << 20, a.stripes, 128, 8
+    for i, place in enumerate(ENC_LEGS):
+        grp = ids[i * n:(i + 1) * n]
+        if not grp:
+            break
+        counters = sorted({c for d in grp for c in eper[d]})
+        avg = {c: sum(eper[d][c] for d in grp) / len(grp) for c in counters}
+        extra = ""
+        if "FETCH_SIZE" in avg:
+            extra += f" read/alg {avg['FETCH_SIZE'] * 1024 * 2 / (S * k * B / ENC_LAUNCHES):.5f}"
+        if "WRITE_SIZE" in avg:
+            extra += f" write/alg {avg['WRITE_SIZE'] * 1024 / (S * np_ * B / ENC_LAUNCHES):.5f}"
+        if "TCC_EA0_RDREQ_LEVEL_sum" in avg and avg.get("TCC_EA0_RDREQ_sum"):
+            extra += f" read level/req {avg['TCC_EA0_RDREQ_LEVEL_sum'] / avg['TCC_EA0_RDREQ_sum']:.1f}"
+        print(f"{place:6s} encode (per launch) " + " ".join(f"{c}={v:.4g}" for c, v in avg.items()) + extra)
 
 
 if __name__ == "__main__":
