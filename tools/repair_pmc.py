@@ -50,6 +50,8 @@ def run(a):
     split.encode()
     torch.cuda.synchronize()
     rep = {"sep": lambda: batch.repair(0, outs), "split": lambda: split.repair(0, out)}
+    d0 = {"sep": lambda: data[0][0], "split": lambda: split.block(0, 0)}
+    ok = True
     for place, sched in LEGS:
         if sched == "auto":
             os.environ.pop("ECW_XOR_SCHED", None)
@@ -64,7 +66,7 @@ def run(a):
         ms = e[0].elapsed_time(e[1]) / a.reps
         print(f"{place:6s} sched {sched:5s} {a.reps} dispatches, {ms:.4f} ms each, "
               f"{S * (r + 1) * B / (ms * 1e-3) / 1e9:.1f} GB/s", flush=True)
-    ok = torch.equal(outs[0], data[0][0]) and torch.equal(out[:B], split.block(0, 0))
+        ok = ok and torch.equal(out[:B], d0[place]())  # (both placements repair into `out`)
     print(f"repairs == D0: {ok}")
     os.environ.pop("ECW_XOR_SCHED", None)
     tiled = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled")
