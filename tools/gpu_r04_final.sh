@@ -28,8 +28,10 @@ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/rtr
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $O/rfetch -o run -- $Q > $O/repair_fetch.log 2>&1 || exit $?
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $O/rwrite -o run -- $Q > $O/repair_write.log 2>&1 || exit $?
 timeout -s KILL 300 rocprofv3 --pmc TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_LEVEL_sum TCC_EA0_RDREQ_DRAM_CREDIT_STALL_sum TCC_TAG_STALL_sum --output-format csv -d $O/rlat -o run -- $Q > $O/repair_lat.log 2>&1 || echo "latency counter pass failed"
+timeout -s KILL 300 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_THRASHING_STALL_sum --output-format csv -d $O/rtlb1 -o run -- $Q > $O/repair_tlb1.log 2>&1 || echo "UTCL1 counter pass failed"
+timeout -s KILL 300 rocprofv3 --pmc GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE --output-format csv -d $O/rtlb2 -o run -- $Q > $O/repair_tlb2.log 2>&1 || echo "UTCL2 counter pass failed"
 cd $R
-for d in rfetch rwrite rlat; do
+for d in rfetch rwrite rlat rtlb1 rtlb2; do
   f=$(find $O/$d -name '*counter_collection.csv' | head -1)
   [ -n "$f" ] && python tools/repair_pmc.py --summarize $f >> $O/repair_pmc_summary.txt 2>&1
 done
