@@ -155,6 +155,22 @@ def test_device_calls_fail_loudly_without_gpu():
     assert ei.value.status == -3
 
 
+@pytest.mark.skipif(E.device_count() > 0, reason="checks the no-GPU failure mode")
+def test_small_host_xors_fail_loudly_without_gpu():
+    """The small host XORs (decodeData, partialDecodeData, repairBlock) that
+    the request service takes on a GPU report ECW_EDEVICE here, never a CPU
+    result; the service counters stay zero and the service is not off."""
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(8, 2, 4, 4096), 1, False)
+    for call in (lambda: c.decodeData([np.zeros(4096, np.uint8)] * c.decodeDataNum, np.zeros(4096, np.uint8)),
+                 lambda: c.partialDecodeData([np.zeros(4096, np.uint8)] * c.partialDecodeNum, np.zeros(4096, np.uint8)),
+                 lambda: c.repairBlock([np.zeros(4096, np.uint8)] * (8 + c.parityNum), 0, np.zeros(4096, np.uint8))):
+        with pytest.raises(E.EcwError) as ei:
+            call()
+        assert ei.value.status == -3
+    assert E.service_counters(0) == {"served": 0, "declined": 0, "epochs": 0, "broken": False}
+    assert _lib.lib.ecw_service_counters(-1, (ctypes.c_uint64 * 4)()) == -1
+
+
 def test_status_strings():
     for st in range(0, -8, -1):
         assert _lib.lib.ecw_status_string(st)
