@@ -68,7 +68,9 @@ def parse(argv=None):
                     help="timed steps of each other single-GPU BASELINE shape (configs1, configs0_shape; 0 = off)")
     ap.add_argument("--host-iters", type=int, default=2,
                     help="rank 0: encodes + repairs of the PCIe-inclusive host-resident leg (0 = off)")
-    ap.add_argument("--chunk-kib", type=int, default=8, help="column piece of the tiled layout")
+    ap.add_argument("--chunk-kib", type=int, default=None,
+                    help="column piece of the tiled layout (default: ecwide_amd.slab.default_chunk(k), 8 KiB at "
+                         "k=128, 16 KiB at k<=32)")
     ap.add_argument("--unit-pad", type=int, default=0, help="tiled layout: padding after each piece run (bytes)")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
@@ -229,7 +231,7 @@ def plan(args, d: Dist, free_bytes: int, parity_num: int, fill: bool = False) ->
         block_mib = args.block_mib if args.block_mib is not None else 64.0
         strong = args.strong
     B = int(block_mib * (1 << 20))
-    align = (args.chunk_kib << 10) if args.layout == "tiled" else 4096
+    align = (chunk_kib(args) << 10) if args.layout == "tiled" else 4096
     share = plan_rank(total, B, d.world, d.rank, strong, per_rank=total, align=align)
     if share["block_bytes"] <= 0:
         raise SystemExit("bench.py: more ranks than column tiles")
@@ -237,10 +239,20 @@ def plan(args, d: Dist, free_bytes: int, parity_num: int, fill: bool = False) ->
     return dict(hbm_fill=fill, strong=strong, stripes_total=stripes_total, block_bytes_full=B, share=share)
 
 
+def chunk_kib(args) -> int:
+    """The tiled layout's column piece of this leg (KiB): --chunk-kib, or the
+    slab's default for k (ecwide_amd/slab.py default_chunk)."""
+    if args.chunk_kib:
+        return args.chunk_kib
+    from ecwide_amd.slab import default_chunk
+
+    return default_chunk(args.k) >> 10
+
+
 def layout_desc(args) -> str:
     return {"blocks": "blocks (each block contiguous, block stride B + 4 KiB, [D.., G.., L..] per stripe)",
             "split": "split (each block contiguous, block stride B + 4 KiB, parity blocks in their own "
-                     "region)"}.get(args.layout, f"tiled ({args.chunk_kib} KiB column pieces: the k data "
+                     "region)"}.get(args.layout, f"tiled ({chunk_kib(args)} KiB column pieces: the k data "
                                                  f"pieces contiguous, parities in their own region)")
 
 
@@ -829,7 +841,7 @@ def device_leg(args, d: Dist, E, pl: dict, k: int, m: int, r: int, steps: int, w
     B, S, s0 = sh["block_bytes"], sh["stripes"], sh["s0"]
     codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, device=d.dev)
     slab = E.StripeSlab(codec, stripes=S, block_bytes=B, device=d.dev, layout=layout,
-                        chunk=args.chunk_kib << 10, unit_pad=args.unit_pad)
+                        chunk=chunk_kib(args) << 10, unit_pad=args.unit_pad)
     out = torch.empty(S * B, dtype=torch.uint8, device=f"cuda:{d.dev}")
     slab.fill_random(seed=args.seed, s0=s0, col_offset=sh["col_offset"])
     torch.cuda.synchronize()
@@ -880,7 +892,7 @@ def pmc_traffic(args, k, r, m, B, S, enc_bytes, launches):
         return None, None
     try:
         pmc = json.load(open(args.pmc))
-        key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{args.chunk_kib}k", "split": "_split"}.get(args.layout, "")
+        key = f"k{k}_r{r}_m{m}_B{B}_S{S}" + {"tiled": f"_tiled{chunk_kib(args)}k", "split": "_split"}.get(args.layout, "")
         ratio = pmc.get(key, {}).get("traffic_over_algorithmic")
         if not ratio:
             return None, None

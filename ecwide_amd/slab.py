@@ -14,7 +14,8 @@ stripes. Three layouts:
   data rows at one stride (the "blocks" slab) cost the encode ~10 %; in a
   region of their own the block layout encodes at the tiled slab's rate
   (tools/rw_layout.py).
-* ``"tiled"``: every block is cut into ``chunk``-byte column pieces; piece c
+* ``"tiled"``: every block is cut into ``chunk``-byte column pieces (default
+  ``default_chunk(k)``: 8 KiB, 16 KiB at k <= 32); piece c
   of the k data blocks of stripe s is one contiguous run of k * chunk bytes
   (data region), piece c of the m + g parities one run in the parity region
   after it. Each (stripe, piece) is encoded as an independent stripe of
@@ -34,6 +35,16 @@ DEFAULT_PAD = 4096
 DEFAULT_CHUNK = 8192
 
 
+def default_chunk(k: int) -> int:
+    """Column piece of the tiled layout for k data blocks. Interleaved on one
+    allocation (tools/layout_ab.py): k = 128 8 KiB (encode 6202 GB/s against
+    5877 at 16 KiB and 5909 at 4 KiB; profiles/r04_k128_piece.log, round 2's
+    sweep agrees); k = 32 16 KiB (CL(32, 8, 2) 16 MiB: encode 6128 / repair 6222
+    against 5986 / 6061 at 8 KiB; CL(32, 11, 3) 64 MiB: 6129 / 5956 against
+    6011 / 6001; 32 KiB and above lose; profiles/r04_k32_piece_cfg1/0.log)."""
+    return 16384 if k <= 32 else DEFAULT_CHUNK
+
+
 # launch_encode (ecw_kernels.hip) windows: 256 CUs x ECW_GRID_PER_CU (256) tiles per launch
 ENCODE_LAUNCH_TILES = 256 * 256
 TICKET_MIN_TILES = 4 * ENCODE_LAUNCH_TILES  # ECW_TICKET_MIN_TILES: one ticket-ordered launch from here on
@@ -42,7 +53,7 @@ TICKET_MIN_TILES = 4 * ENCODE_LAUNCH_TILES  # ECW_TICKET_MIN_TILES: one ticket-o
 class StripeSlab:
     def __init__(self, codec: NativeCodec, stripes: int, block_bytes: int | None = None,
                  pad: int = DEFAULT_PAD, device: int | None = None, layout: str = "blocks",
-                 chunk: int = DEFAULT_CHUNK, unit_pad: int = 0, base_offset: int = 0):
+                 chunk: int | None = None, unit_pad: int = 0, base_offset: int = 0):
         import torch
 
         self.codec = codec
@@ -64,6 +75,10 @@ class StripeSlab:
             self.parity_offset = stripes * self.stripe_stride
             nbytes = self.parity_offset + stripes * self.pstripe_stride
         elif layout == "tiled":
+            if chunk is None:
+                chunk = default_chunk(k)
+                while self.len % chunk and chunk > 256:  # blocks that are not a multiple of the piece
+                    chunk //= 2
             if chunk % 256 or chunk <= 0 or self.len % chunk:
                 raise ValueError("tiled layout: chunk must be a positive multiple of 256 dividing the block size")
             if unit_pad % 256:

@@ -923,11 +923,11 @@ def test_literal_mode_slab_writes_zero_locals(E, torch, orc, k, m, r):
             assert not L.any()
 
 
-def full_digest_case(E, torch, name, manifest):
+def full_digest_case(E, torch, name, manifest, layout="blocks"):
     e = next(x for x in manifest["full"] if x["name"] == name)
     k, m, r, B = e["k"], e["m"], e["r"], e["len"]
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
-    slab = E.StripeSlab(c, stripes=1, block_bytes=B)
+    slab = E.StripeSlab(c, stripes=1, block_bytes=B, layout=layout)  # tiled: the default piece for k
     slab.fill_random(seed=e["seed"])
     slab.encode()
     out = torch.empty(B, dtype=torch.uint8, device="cuda")
@@ -950,6 +950,17 @@ def test_full_cfg3_k128_64MiB_digests(E, torch, manifest):
 
 def test_full_cfg1_k32_64MiB_digests(E, torch, manifest):
     full_digest_case(E, torch, "cfg1_full", manifest)
+
+
+@pytest.mark.parametrize("name", ["cfg1_full", "cfg2_full"])
+def test_full_k32_digests_tiled_default_piece(E, torch, manifest, name):
+    """The k = 32 BASELINE shapes in the tiled slab at its default piece for
+    k = 32 (16 KiB, ecwide_amd/slab.py default_chunk; the bench's configs1 /
+    configs0_shape legs): the same full-size digests as the block layout."""
+    from ecwide_amd.slab import default_chunk
+
+    assert default_chunk(32) == 16384
+    full_digest_case(E, torch, name, manifest, layout="tiled")
 
 
 def test_linearity_full_size(E, torch):
