@@ -91,6 +91,7 @@ struct EncodeGeom {
   FastDiv per;           // column tiles per stripe in that numbering
   unsigned long long* ticket;  // non-null: workgroups take tiles in order from this counter (zeroed before the launch)
   uint32_t wmask, wwidth;      // write window (asm tile): store when (clock & wmask) < wwidth; 0 = off
+  uint32_t remap;              // 1: per-XCD contiguous tile order (wg_slot)
 };
 
 // Launchers return hipSuccess or the launch error (an earlier, unrelated HIP
@@ -148,6 +149,7 @@ struct XorSched {
   FastDiv ns;             // stripes (order 1)
   uint32_t order;         // 0: groups numbered stripe-major, 1: column-major
   uint32_t wmask, wwidth; // write window: store when (clock & wmask) < wwidth; 0 = off
+  uint32_t remap;         // 1: per-XCD contiguous group order (wg_slot)
 };
 hipError_t launch_xor_ptr(const XorPtr& p, const XorGeom& g, hipStream_t s);
 hipError_t launch_xor_slab(const XorSlab& p, const XorGeom& g, hipStream_t s);

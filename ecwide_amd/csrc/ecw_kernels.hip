@@ -232,18 +232,20 @@ __device__ __forceinline__ uint4 unpack_row(const uint32_t (&acc)[16 * NW], int 
   return make_uint4(o[0], o[1], o[2], o[3]);
 }
 
-#ifndef ECW_XCD_REMAP
-#define ECW_XCD_REMAP 0  // 1: blocks b and b + 8 (one XCD) take neighbouring tiles (tuning)
-#endif
 // First tile of this workgroup's grid-stride walk. Blocks are dealt round-robin
-// over the 8 XCDs; with the remap each XCD walks its own contiguous 1/8 of
-// every grid-sized window (a permutation of [0, gridDim.x) when 8 divides it).
-__device__ __forceinline__ uint64_t wg_slot() {
-#if ECW_XCD_REMAP
+// over the 8 XCDs; with `remap` each XCD walks its own contiguous 1/8 of every
+// grid-sized window (a permutation of [0, gridDim.x) when 8 divides it), so
+// the workgroups resident on one CU take tiles 32 apart instead of 256 and
+// share more address translations (EncodeGeom::remap, XorSched::remap).
+__device__ __forceinline__ uint64_t wg_slot(uint32_t remap = 0) {
   const uint32_t G = gridDim.x, b = blockIdx.x;
-  if ((G & 7u) == 0) return static_cast<uint64_t>(b & 7u) * (G >> 3) + (b >> 3);
-#endif
+  if (remap && (G & 7u) == 0) return static_cast<uint64_t>(b & 7u) * (G >> 3) + (b >> 3);
   return blockIdx.x;
+}
+// ECW_XCD_REMAP = 0 | 1 (tuning; read per launch): the per-XCD tile order above
+inline uint32_t xcd_remap_env() {
+  const char* e = std::getenv("ECW_XCD_REMAP");
+  return e && e[0] == '1' ? 1u : 0u;
 }
 
 // Column tile `tile` of the slab: stripe, this lane's column, whole tile in range?
@@ -486,7 +488,7 @@ __global__ __launch_bounds__(kBlock * asm_tpb<NW>(), NW == 1   ? ECW_ASM_MIN_WAV
   // and no compiler-issued memory operation drains the ring between tiles.
   // Every wave runs every iteration (take_ticket holds a barrier); a wave whose
   // tile is past the end skips the work.
-  for (uint32_t t0 = tickets ? take_ticket(g, slot, TPB) : g.tile_begin + static_cast<uint32_t>(wg_slot()) * TPB;
+  for (uint32_t t0 = tickets ? take_ticket(g, slot, TPB) : g.tile_begin + static_cast<uint32_t>(wg_slot(g.remap)) * TPB;
        t0 < g.tile_end; t0 = tickets ? take_ticket(g, slot, TPB) : t0 + gridDim.x * TPB) {
     const uint32_t tile = t0 + half;
     if (tile >= g.tile_end) continue;
@@ -687,7 +689,7 @@ __device__ __forceinline__ void xor_tiles_fixed(const Args& a, const XorGeom& g,
 template <int N, int K, class Args>
 __global__ __launch_bounds__(kBlock) void xor_kernel_fixed(const Args a, const XorGeom g, const XorSched sc) {
   const uint32_t total = static_cast<uint32_t>(g.stripes) * sc.per.d;
-  for (uint32_t grp = static_cast<uint32_t>(wg_slot()); grp < total; grp += gridDim.x) {
+  for (uint32_t grp = static_cast<uint32_t>(wg_slot(sc.remap)); grp < total; grp += gridDim.x) {
     uint32_t s, c;
     if (sc.order) {
       c = fast_div(grp, sc.ns);
@@ -1001,6 +1003,7 @@ hipError_t launch_encode_range(const Rows& rows, const EncodeGeom& g0, const uin
   if (g0.stripes < 0 || total >= kMaxTilesPerLaunch || per > 0xFFFFFFFFull) return hipErrorInvalidValue;
   EncodeGeom gw = g0;
   set_write_window(rows, gw);
+  gw.remap = xcd_remap_env();
   gw.per = make_fastdiv(static_cast<uint32_t>(per ? per : 1));
   gw.ticket = nullptr;
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
@@ -1136,6 +1139,7 @@ hipError_t launch_xor_skew(const Args& a, const XorGeom& g, const XorChoice& c, 
   sc.per = make_fastdiv(static_cast<uint32_t>(per));
   sc.ns = make_fastdiv(static_cast<uint32_t>(g.stripes > 0 ? g.stripes : 1));
   sc.order = c.order;
+  sc.remap = xcd_remap_env();
   sc.wmask = (1u << c.log2p) - 1;
   sc.wwidth = c.wwidth;
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR));

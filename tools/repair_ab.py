@@ -13,7 +13,8 @@ Placements (S stripes of CL(k, r, m), B-byte blocks):
   carved4k  the same at block stride B + 4 KiB
 Schedules (ECW_XOR_SCHED = "K,ORDER[,LOG2P,W]", ecw_kernels.hip launch_xor_range):
   K tiles per workgroup read diagonally, ORDER 1 = column-major groups,
-  LOG2P,W = write window.
+  LOG2P,W = write window; "auto" = the library's choice; a "+r" suffix (also on
+  --enc-windows settings) adds the per-XCD tile order (ECW_XCD_REMAP=1).
 
   python tools/repair_ab.py --lib build/variants/skewall.so [--stripes 4] [--scheds 1,0 4,0 ...]
 """
@@ -152,10 +153,15 @@ def main():
         order = combos[rd % len(combos):] + combos[:rd % len(combos)]
         for p, sc in order:
             enc, rep, d0 = legs[p]
-            if sc == "auto":
+            base, _, rflag = sc.partition("+")  # "+r": the per-XCD tile order (ECW_XCD_REMAP=1)
+            if rflag == "r":
+                os.environ["ECW_XCD_REMAP"] = "1"
+            else:
+                os.environ.pop("ECW_XCD_REMAP", None)
+            if base == "auto":
                 os.environ.pop("ECW_XOR_SCHED", None)  # the library's own choice
             else:
-                os.environ["ECW_XOR_SCHED"] = sc
+                os.environ["ECW_XOR_SCHED"] = base
             assert rep() == 0
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
@@ -172,10 +178,16 @@ def main():
             if a.encode and sc == a.scheds[0]:
                 rr[1].append(enc_bytes * a.iters / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9)
                 for wv in a.enc_windows:  # the encode under other write-window settings, same round
-                    if wv == "auto":
-                        os.environ.pop("ECW_WRITE_WINDOW", None)
+                    wbase, _, rflag = wv.partition("+")
+                    if rflag == "r":
+                        os.environ["ECW_XCD_REMAP"] = "1"
                     else:
-                        os.environ["ECW_WRITE_WINDOW"] = wv
+                        os.environ.pop("ECW_XCD_REMAP", None)
+                    if wbase == "auto":
+                        os.environ.pop("ECW_WRITE_WINDOW", None)
+                os.environ.pop("ECW_XCD_REMAP", None)
+                    else:
+                        os.environ["ECW_WRITE_WINDOW"] = wbase
                     f = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                     enc()
                     f[0].record()
