@@ -185,7 +185,6 @@ def main():
                         os.environ.pop("ECW_XCD_REMAP", None)
                     if wbase == "auto":
                         os.environ.pop("ECW_WRITE_WINDOW", None)
-                os.environ.pop("ECW_XCD_REMAP", None)
                     else:
                         os.environ["ECW_WRITE_WINDOW"] = wbase
                     f = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
@@ -197,6 +196,7 @@ def main():
                     torch.cuda.synchronize()
                     encw.setdefault((p, wv), []).append(enc_bytes * a.iters / (f[0].elapsed_time(f[1]) * 1e-3) / 1e9)
                 os.environ.pop("ECW_WRITE_WINDOW", None)
+                os.environ.pop("ECW_XCD_REMAP", None)
             if rd == 0:
                 ok = all(torch.equal(out[s * B:(s + 1) * B], d0[s]()) for s in range(S))
                 if not ok:
