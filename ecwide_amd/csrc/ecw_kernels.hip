@@ -242,10 +242,12 @@ __device__ __forceinline__ uint64_t wg_slot(uint32_t remap = 0) {
   if (remap && (G & 7u) == 0) return static_cast<uint64_t>(b & 7u) * (G >> 3) + (b >> 3);
   return blockIdx.x;
 }
-// ECW_XCD_REMAP = 0 | 1 (tuning; read per launch): the per-XCD tile order above
-inline uint32_t xcd_remap_env() {
+// ECW_XCD_REMAP = 0 | 1 (tuning; read per launch) overrides the launcher's
+// choice of the per-XCD tile order above
+inline uint32_t xcd_remap_env(uint32_t dflt) {
   const char* e = std::getenv("ECW_XCD_REMAP");
-  return e && e[0] == '1' ? 1u : 0u;
+  if (!e || !e[0]) return dflt;
+  return e[0] == '1' ? 1u : 0u;
 }
 
 // Column tile `tile` of the slab: stripe, this lane's column, whole tile in range?
@@ -966,6 +968,20 @@ inline bool window_auto(const SlabRows&, const EncodeGeom& g) { return window_sh
 inline bool window_auto(const PtrRows&, const EncodeGeom& g) { return window_shape(g); }
 inline bool window_auto(const PtrTabRows&, const EncodeGeom& g) { return window_shape(g); }
 
+// Tile order of the encode: the per-XCD contiguous order (wg_slot) for blocks
+// behind pointers (the caller's own allocations). Their encode keeps the
+// address-translation path busy (UTCL2 busy 96 % of the launch over 1088
+// separate 64 MiB allocations, 93 % on the split slab, 4 % on the tiled slab;
+// separate allocations take 2x the split slab's UTCL1 misses:
+// profiles/r04b_repair_pmc_summary.txt); with the remap the workgroups
+// resident on a CU take tiles 128 KiB apart instead of 1 MiB and share more
+// translations. Interleaved (profiles/r04_remap_1/2.log): separate blocks
+// 6012 -> 6211 and 5932 -> 6136 GB/s; slabs within +-1 %, so they keep the
+// dispatch order.
+inline uint32_t remap_auto(const SlabRows&) { return 0; }
+inline uint32_t remap_auto(const PtrRows&) { return 1; }
+inline uint32_t remap_auto(const PtrTabRows&) { return 1; }
+
 template <class Rows>
 void set_write_window(const Rows& rows, EncodeGeom& g) {
   uint32_t log2p = 11, w = 64;
@@ -1003,7 +1019,7 @@ hipError_t launch_encode_range(const Rows& rows, const EncodeGeom& g0, const uin
   if (g0.stripes < 0 || total >= kMaxTilesPerLaunch || per > 0xFFFFFFFFull) return hipErrorInvalidValue;
   EncodeGeom gw = g0;
   set_write_window(rows, gw);
-  gw.remap = xcd_remap_env();
+  gw.remap = xcd_remap_env(remap_auto(rows));
   gw.per = make_fastdiv(static_cast<uint32_t>(per ? per : 1));
   gw.ticket = nullptr;
   const uint64_t win = ECW_COHORT_TILES > 0    ? static_cast<uint64_t>(ECW_COHORT_TILES)
@@ -1139,7 +1155,7 @@ hipError_t launch_xor_skew(const Args& a, const XorGeom& g, const XorChoice& c, 
   sc.per = make_fastdiv(static_cast<uint32_t>(per));
   sc.ns = make_fastdiv(static_cast<uint32_t>(g.stripes > 0 ? g.stripes : 1));
   sc.order = c.order;
-  sc.remap = xcd_remap_env();
+  sc.remap = xcd_remap_env(0);  // the XOR: -0.4..-5 % with it (profiles/r04_remap_*.log)
   sc.wmask = (1u << c.log2p) - 1;
   sc.wwidth = c.wwidth;
   const dim3 grid(grid_for(total, ECW_GRID_PER_CU_XOR));

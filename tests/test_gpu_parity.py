@@ -388,6 +388,41 @@ def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, lay
             assert np.array_equal(outs["on"][n][i][B - W:].cpu().numpy(), w), (s, i)
 
 
+@pytest.mark.parametrize("remap", ["0", "1", None])
+def test_xcd_remap_same_bytes(E, torch, orc, monkeypatch, remap):
+    """The per-XCD tile order (ECW_XCD_REMAP; default on for pointer-table
+    encodes, off elsewhere) only permutes which workgroup takes which tile:
+    pointer-table encode and repair, and the split slab's encode, give the
+    oracle's bytes with it on, off and at the default, with a grid that is and
+    one that is not a multiple of 8 workgroups."""
+    if remap is None:
+        monkeypatch.delenv("ECW_XCD_REMAP", raising=False)
+    else:
+        monkeypatch.setenv("ECW_XCD_REMAP", remap)
+    k, m, r = 64, 3, 16
+    for B, S in ((1 << 20, 32), (3 * 4096 + 64, 5)):  # 8192 tiles; 20 tiles (+ ragged)
+        c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+        src = E.StripeSlab(c, stripes=S, block_bytes=B, layout="split")
+        src.fill_random(seed=33)
+        src.encode()
+        data = [[src.block(s, j).clone() for j in range(k)] for s in range(S)]
+        par = [[torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(c.parityNum)] for _ in range(S)]
+        batch = E.BlockBatch(c, data, par)
+        batch.encode()
+        out = [torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(S)]
+        batch.repair(0, out)
+        torch.cuda.synchronize()
+        W = min(8192, B)
+        oc = orc.codec("C", k, m, r, W)
+        for s in (0, S - 1):
+            for i in range(c.parityNum):
+                assert torch.equal(par[s][i], src.parity(s)[i]), (B, s, i)
+            want = oc.encode([orc.fill(W, 33, s, j, B - W) for j in range(k)])
+            for i, w in enumerate(want):
+                assert np.array_equal(par[s][i][B - W:].cpu().numpy(), w), (B, s, i)
+            assert torch.equal(out[s], data[s][0]), (B, s)
+
+
 def test_full_size_tiled_bench_path(E, torch, manifest):
     """The bench's timed bytes at the bench's size: tiled slab, CL(128, 27, 3),
     64 MiB blocks, 8 stripes, seed 103. Stripe 0 is the stripe of manifest
