@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--r", type=int, default=27)
     ap.add_argument("--mib", type=int, default=64)
     ap.add_argument("--stripes", type=int, default=4)
+    ap.add_argument("--chunk", type=int, default=8192, help="column piece of the tiled placement")
     ap.add_argument("--placements", default="tiled,split,sep,carved0,carved4k")
     ap.add_argument("--scheds", nargs="+", default=["1,0", "4,0", "1,1", "4,1", "1,0,11,64", "2,0", "8,0"])
     ap.add_argument("--rounds", type=int, default=4)
@@ -85,7 +86,7 @@ def main():
     for p in a.placements.split(","):
         if p in ("tiled", "split"):
             if p == "tiled":
-                ch = 8192
+                ch = a.chunk
                 units = S * (B // ch)
                 dbuf = torch.empty(units * k * ch, dtype=torch.uint8, device="cuda")
                 pbuf = torch.empty(units * np_ * ch, dtype=torch.uint8, device="cuda")
