@@ -1125,9 +1125,15 @@ struct XorChoice {
 //  * the tiled slab's 8 KiB units keep K = 1 and no window (K = 4: -0.5..-8 %,
 //    window -2..-70 %: its sources are one contiguous run already).
 // Column-major group order and K = 2 / 8 gained less than K = 4 everywhere.
+//  * round 4, later: the tiled slab's 16 KiB units (k <= 32, slab.default_chunk)
+//    are one whole group of K = 4 tiles and take the same schedule: CL(32, 8, 2)
+//    6240 -> 6379, CL(32, 11, 3) 6259 -> 6537 GB/s (profiles/r04_k32r_cfg1/0.log);
+//    K = 2 on the 8 KiB units of k = 128: +0.5 % with the window, -2 % without
+//    (r04_k128r_tiled.log), so they keep K = 1.
 template <class Args>
 inline XorChoice xor_choice(const XorGeom& g) {
-  const bool whole = g.len >= 65536;
+  constexpr uint64_t group = static_cast<uint64_t>(ECW_XOR_SKEW_K) * kTileBytes;
+  const bool whole = g.len >= 65536 || (g.len >= group && g.len % group == 0);
   XorChoice c{whole ? ECW_XOR_SKEW_K : 1, 0, 11, 0};
   if (whole && g.n >= 8 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192) c.wwidth = 64;
   if (const char* e = std::getenv("ECW_XOR_SCHED")) {

@@ -179,7 +179,8 @@ def test_split_layout_encode_vs_oracle(E, torch, orc, k, m, r, B, S, tiled):
 
 
 @pytest.mark.parametrize("k,m,r,B,S,chunk", [(128, 3, 27, 1 << 16, 2, 8192), (32, 6, 8, 4 * 4096, 2, 4096),
-                                              (20, 2, 5, 3 * 8192, 3, 8192)])
+                                              (20, 2, 5, 3 * 8192, 3, 8192),
+                                              (32, 2, 8, 4 * 16384, 3, 16384)])  # k <= 32 default: K = 4 repair groups
 def test_tiled_slab_encode_repair(E, torch, orc, k, m, r, B, S, chunk):
     """StripeSlab(layout="tiled"): every (stripe, piece) unit vs the oracle, and
     the split-layout repair of every D and L block rebuilds it exactly."""
