@@ -470,9 +470,11 @@ def other_layouts(args, E, codec, slab, S, B, out, enc_bytes, rep_bytes, dev) ->
     desc = {
         "tiled": "tiled slab (the headline layout)",
         "split": "split slab: whole blocks (stride B + 4 KiB), the data blocks of all stripes then their parity "
-                 "blocks (ecw_encode_batch_split_dev)",
+                 "blocks (ecw_encode_batch_split_dev; encode with the write window, repair with the K=4 diagonal "
+                 "XOR schedule + write window: DESIGN.md 4.1, 4.2)",
         "pointer": f"pointer tables: {S * (k + np_)} separately allocated {B >> 20} MiB blocks, one "
-                   f"ecw_encode_ptrs_dev / ecw_xor_reduce_ptrs_dev launch over the {S} stripes",
+                   f"ecw_encode_ptrs_dev / ecw_xor_reduce_ptrs_dev launch over the {S} stripes (encode with the "
+                   f"per-XCD tile order + write window, repair with the K=4 diagonal XOR schedule + write window)",
     }
     res = {"interleaved": f"{rounds} rounds x (tiled, split, pointer) x {n2} encodes + {n2} repairs, one process"}
     for name, (en, rp) in rates.items():
