@@ -148,13 +148,11 @@ class Dist:
             # rehearsal of the N>1 path) ranks share devices over gloo
             self.dev = self.local % self.ndev
             torch.cuda.set_device(self.dev)
-        self.distinct = self.dry or self.ndev >= self.world
+        self.distinct = self.dry or self.ndev >= self.world  # refined below from the ranks' PCI ids
         if self.world > 1:
             import torch
             import torch.distributed as dist
 
-            if not self.distinct:
-                print(f"bench.py: rehearsal: {self.world} ranks share {self.ndev} GPU(s)", file=sys.stderr)
             # no stripe byte moves between ranks: the only collectives are the
             # barriers around the timed region and a few scalars (max time, min
             # block size, verification), so they run on gloo over loopback --
@@ -162,10 +160,20 @@ class Dist:
             dist.init_process_group("gloo")
             self.backend = dist.get_backend()
             if not self.dry:
-                # one process per GPU: with enough GPUs every rank must sit on its own
-                devs = self.gather(float(torch.cuda.current_device()))
-                if self.distinct and len(set(devs)) != self.world:
-                    raise SystemExit(f"bench.py: ranks share GPUs {devs} although {self.ndev} are visible")
+                # one process per GPU: which physical GPU each rank drives (PCI
+                # domain / bus / device), so the line is right whether every rank
+                # sees all GPUs or only its own (per-rank visibility)
+                pr = torch.cuda.get_device_properties(self.dev)
+                key = float(getattr(pr, "pci_domain_id", 0) * 65536 + getattr(pr, "pci_bus_id", 0) * 256
+                            + getattr(pr, "pci_device_id", 0)) if hasattr(pr, "pci_bus_id") else None
+                if key is not None:
+                    phys = self.gather(key)
+                    self.distinct = len(set(phys)) == self.world
+                    if self.ndev >= self.world and not self.distinct:
+                        raise SystemExit(f"bench.py: ranks share GPUs {phys} although {self.ndev} are visible")
+                if not self.distinct and self.rank == 0:
+                    print(f"bench.py: rehearsal: {self.world} ranks share GPUs ({self.ndev} visible per rank)",
+                          file=sys.stderr)
 
     def _tensor(self, vals):
         import torch
