@@ -49,6 +49,11 @@ class ecw_codec_info(Structure):
     ]
 
 
+class ecw_schedule(Structure):
+    _fields_ = [(name, c_int) for name in ("xor_skew", "xor_order", "xor_window_log2p", "xor_window_width",
+                                           "enc_window_log2p", "enc_window_width", "xcd_remap")]
+
+
 _u8p = POINTER(c_uint8)
 _pp = POINTER(c_void_p)
 
@@ -91,6 +96,8 @@ SIGNATURES = {
                                      c_size_t, c_void_p]),
     "ecw_repair_sources": (c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     "ecw_service_counters": (c_int, [c_int, POINTER(c_uint64)]),
+    "ecw_set_schedule": (c_int, [POINTER(ecw_schedule)]),
+    "ecw_get_schedule": (c_int, [POINTER(ecw_schedule)]),
     "ecw_fill_random_dev": (c_int, [c_int, c_void_p, c_size_t, c_size_t, c_int, c_int, c_size_t, c_uint64, c_int,
                                     c_int, c_void_p]),
     "ecw_fill_random_pieces_dev": (c_int, [c_int, c_void_p, c_size_t, c_size_t, c_int, c_int, c_size_t, c_size_t,

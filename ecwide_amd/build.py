@@ -10,15 +10,18 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(HERE)
-SOURCES = [os.path.join(HERE, "csrc", "ecw_codec.cpp"), os.path.join(HERE, "csrc", "ecw_kernels.hip")]
-HEADERS = [os.path.join(HERE, "csrc", f) for f in ("ecw_gf.hpp", "ecw_internal.hpp", "ecw_encode_asm.hpp")] + [
+SOURCES = [os.path.join(HERE, "csrc", f) for f in
+           ("ecw_codec.cpp", "ecw_kernels.hip", "ecw_xor_ptr.hip", "ecw_xor_slab.hip", "ecw_service.hip")]
+HEADERS = [os.path.join(HERE, "csrc", f) for f in
+           ("ecw_gf.hpp", "ecw_internal.hpp", "ecw_tuning.hpp", "ecw_device.hpp", "ecw_encode_asm.hpp", "ecw_xor.hpp")] + [
     os.path.join(REPO, "include", "ecwide.h")]
 OUT = os.path.join(HERE, "libecwide.so")
+OBJ = os.path.join(REPO, "build", "obj")
 SHIM_SRC = os.path.join(HERE, "csrc", "ecw_isal_shim.cpp")
 SHIM_OUT = os.path.join(HERE, "libecw_isal.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-FLAGS = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wmissing-field-initializers", "-Wno-unused-function",
-         "-I" + os.path.join(REPO, "include")]
+FLAGS_C = ["--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wmissing-field-initializers",
+           "-Wno-unused-function", "-I" + os.path.join(REPO, "include")]
 
 
 def _tmp() -> str:
@@ -34,11 +37,31 @@ def up_to_date(out=OUT, sources=SOURCES) -> bool:
     return all(os.path.getmtime(p) <= t for p in sources + HEADERS + [__file__])
 
 
+def compile_lib(out: str, extra=(), obj_dir: str = OBJ) -> None:
+    """Every translation unit to an object in parallel (the kernel TUs take
+    minutes each: encode, XOR and service are separate so they compile side
+    by side), then one link; `extra` flags (a tuning variant's -D...) apply
+    to every TU."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    os.makedirs(obj_dir, exist_ok=True)
+
+    def one(src):
+        o = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        cmd = [HIPCC, *FLAGS_C, *extra, "-c", src, "-o", o + _tmp()]
+        subprocess.run(cmd, check=True)
+        os.replace(o + _tmp(), o)
+        return o
+
+    with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
+        objs = list(ex.map(one, SOURCES))
+    subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out + _tmp()], check=True)
+    os.replace(out + _tmp(), out)
+
+
 def build(force: bool = False) -> str:
     if force or not up_to_date():
-        cmd = [HIPCC, *FLAGS, *SOURCES, "-o", OUT + _tmp()]
-        subprocess.run(cmd, check=True)
-        os.replace(OUT + _tmp(), OUT)
+        compile_lib(OUT)
     if force or not up_to_date(SHIM_OUT, [SHIM_SRC, OUT]):
         # host-only C++; links libecwide.so next to it ($ORIGIN)
         cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-I" + os.path.join(REPO, "include"),

@@ -361,3 +361,51 @@ def service_counters(device: int = 0) -> dict:
     out = (c_uint64 * 4)()
     _check(lib.ecw_service_counters(device, out), "service_counters")
     return {"served": out[0], "declined": out[1], "epochs": out[2], "broken": bool(out[3])}
+
+
+SCHEDULE_FIELDS = ("xor_skew", "xor_order", "xor_window_log2p", "xor_window_width", "enc_window_log2p",
+                   "enc_window_width", "xcd_remap")
+
+
+def get_schedule() -> dict:
+    """The process's launch schedule (ecwide.h ecw_schedule; -1 = the library's
+    per-layout choice)."""
+    s = _lib.ecw_schedule()
+    _check(lib.ecw_get_schedule(byref(s)), "get_schedule")
+    return {f: getattr(s, f) for f in SCHEDULE_FIELDS}
+
+
+def set_schedule(**fields) -> dict:
+    """Set the launch schedule: every field not given goes back to -1 (auto).
+    Returns the previous schedule. Tuning only: no field changes a result byte."""
+    bad = set(fields) - set(SCHEDULE_FIELDS)
+    if bad:
+        raise TypeError(f"unknown schedule fields {sorted(bad)}")
+    prev = get_schedule()
+    s = _lib.ecw_schedule(*[int(fields.get(f, -1)) for f in SCHEDULE_FIELDS])
+    _check(lib.ecw_set_schedule(byref(s)), f"set_schedule({fields})")
+    return prev
+
+
+def parse_schedule(xor: str | None = None, window: str | None = None, remap: str | None = None) -> dict:
+    """Schedule fields from the string forms the tools and the environment use:
+    xor = "K,ORDER[,LOG2P,W]" (a whole XOR schedule: no window unless given),
+    window = "off" | "on" | "LOG2P,W" (the encode's write window), remap = "0" | "1"."""
+    f = {}
+    if xor not in (None, "auto"):
+        v = [int(x) for x in xor.split(",")]
+        f["xor_skew"], f["xor_window_width"] = v[0], 0
+        if len(v) >= 2:
+            f["xor_order"] = v[1]
+        if len(v) >= 4:
+            f["xor_window_log2p"], f["xor_window_width"] = v[2], v[3]
+    if window not in (None, "auto"):
+        if window in ("off", "0"):
+            f["enc_window_width"] = 0
+        elif window == "on":
+            f["enc_window_log2p"], f["enc_window_width"] = 11, 64
+        else:
+            f["enc_window_log2p"], f["enc_window_width"] = (int(x) for x in window.split(","))
+    if remap not in (None, "auto"):
+        f["xcd_remap"] = int(remap)
+    return f

@@ -471,12 +471,127 @@ bool all_aligned(P const* ptrs, int n) {
   return true;
 }
 
+// ---- launch schedule (ecw_set_schedule) ------------------------------------
+constexpr int kWindowLog2p = 11, kWindowWidth = 64;  // a window with one field given: the other's default
+
+bool skew_built(int k) {
+  for (int s : kXorSkews)
+    if (s == k) return true;
+  return false;
+}
+
+// every field -1 or in range; windows completed with the defaults
+bool normalise(Schedule& s) {
+  auto in = [](int v, int lo, int hi) { return v == -1 || (v >= lo && v <= hi); };
+  if (!(s.xor_skew == -1 || skew_built(s.xor_skew)) || !in(s.xor_order, 0, 1) || !in(s.xcd_remap, 0, 1) ||
+      !in(s.xor_log2p, 4, 24) || !in(s.enc_log2p, 4, 24) || !in(s.xor_width, 0, 1 << 24) ||
+      !in(s.enc_width, 0, 1 << 24))
+    return false;
+  for (auto w : {std::make_pair(&s.xor_log2p, &s.xor_width), std::make_pair(&s.enc_log2p, &s.enc_width)}) {
+    if (*w.first == -1 && *w.second > 0) *w.first = kWindowLog2p;
+    if (*w.first != -1 && *w.second == -1) *w.second = kWindowWidth;
+  }
+  return true;
+}
+
+// The environment's overrides, read once (tuning runs that predate the API):
+// ECW_XOR_SCHED = "K,ORDER[,LOG2P,W]" names the whole XOR schedule (no window
+// unless given), ECW_WRITE_WINDOW = off | on | "LOG2P,W" the encode's window,
+// ECW_XCD_REMAP = 0 | 1 the tile order of both. A malformed or out-of-range
+// value is reported on stderr and ignored.
+Schedule schedule_from_env() {
+  Schedule s{-1, -1, -1, -1, -1, -1, -1};
+  auto warn = [](const char* var, const char* v) {
+    std::fprintf(stderr, "libecwide: ignoring %s=%s (out of range or not built)\n", var, v);
+  };
+  if (const char* e = std::getenv("ECW_XOR_SCHED")) {
+    Schedule t = s;
+    int k = 1;
+    unsigned o = 0, lp = 0, w = 0;
+    const int got = std::sscanf(e, "%d,%u,%u,%u", &k, &o, &lp, &w);
+    if (got >= 1) {
+      t.xor_skew = k;
+      t.xor_width = 0;
+      if (got >= 2) t.xor_order = static_cast<int>(o);
+      if (got >= 4) {
+        t.xor_log2p = static_cast<int>(lp);
+        t.xor_width = static_cast<int>(w);
+      }
+    }
+    if (got >= 1 && got != 3 && normalise(t))
+      s = t;
+    else
+      warn("ECW_XOR_SCHED", e);
+  }
+  if (const char* e = std::getenv("ECW_WRITE_WINDOW")) {
+    Schedule t = s;
+    unsigned a = 0, b = 0;
+    if (!std::strcmp(e, "off") || !std::strcmp(e, "0")) {
+      t.enc_width = 0;
+    } else if (!std::strcmp(e, "on")) {
+      t.enc_log2p = kWindowLog2p;
+      t.enc_width = kWindowWidth;
+    } else if (std::sscanf(e, "%u,%u", &a, &b) == 2) {
+      t.enc_log2p = static_cast<int>(a);
+      t.enc_width = static_cast<int>(b);
+    } else if (e[0]) {
+      t.enc_log2p = -2;  // rejected below
+    }
+    if (normalise(t))
+      s = t;
+    else
+      warn("ECW_WRITE_WINDOW", e);
+  }
+  if (const char* e = std::getenv("ECW_XCD_REMAP")) {
+    if (e[0] == '0' || e[0] == '1')
+      s.xcd_remap = e[0] - '0';
+    else if (e[0])
+      warn("ECW_XCD_REMAP", e);
+  }
+  return s;
+}
+
+std::mutex g_sched_mu;
+Schedule g_sched;
+bool g_sched_init = false;
+
+Schedule& schedule_locked() {
+  if (!g_sched_init) {
+    g_sched = schedule_from_env();
+    g_sched_init = true;
+  }
+  return g_sched;
+}
+
 }  // namespace
+
+Schedule ecw::current_schedule() {
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  return schedule_locked();
+}
 
 // =====================================================================
 extern "C" {
 
 int ecw_abi_version(void) { return ECW_ABI_VERSION; }
+
+int ecw_set_schedule(const ecw_schedule* in) {
+  Schedule s{-1, -1, -1, -1, -1, -1, -1};
+  if (in)
+    s = Schedule{in->xor_skew,         in->xor_order,        in->xor_window_log2p, in->xor_window_width,
+                 in->enc_window_log2p, in->enc_window_width, in->xcd_remap};
+  if (!normalise(s)) return ECW_EINVAL;
+  std::lock_guard<std::mutex> lk(g_sched_mu);
+  schedule_locked() = s;
+  return ECW_OK;
+}
+
+int ecw_get_schedule(ecw_schedule* out) {
+  if (!out) return ECW_EINVAL;
+  const Schedule s = current_schedule();
+  *out = ecw_schedule{s.xor_skew, s.xor_order, s.xor_log2p, s.xor_width, s.enc_log2p, s.enc_width, s.xcd_remap};
+  return ECW_OK;
+}
 
 const char* ecw_status_string(int status) {
   switch (status) {
@@ -1071,8 +1186,8 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
   if (len == 0) return ECW_OK;
   // a small XOR (decodeData / partialDecodeData / repair / xorIntemediate of
   // blocks up to 64 KiB): the resident request service, no launch
-  const bool small = len <= kSvcMaxLen;
-  if (small && op == op_xor && nout == 1) {
+  const bool offered = len <= kSvcMaxLen && op == op_xor && nout == 1;
+  if (offered) {
     const int sst = svc::serve(c, in, nin, out, len, true);
     if (sst != svc::kNotServed) return sst;
   }
@@ -1082,9 +1197,13 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
   DeviceGuard g(c->device);
   if (!g.ok) return ECW_EDEVICE;
   // bulk work is not queued behind the request service's resident kernel (its
-  // launches also ask a running epoch to leave); a small call the service did
-  // not take does not hold it off in turn
-  svc::Hold hold(c->device, !small);
+  // launches also ask a running epoch to leave). A small XOR the service
+  // declined (it was held off or stopping) does not hold it off in turn;
+  // every other call -- bulk, a small op_zero, an XOR of more sources than
+  // the service takes -- does, so it never waits out a running epoch on a
+  // shared hardware queue.
+  svc::Hold hold(c->device, !offered);
+  if (offered) svc::yield(c->device, false);
   if (!c->pipe) {
     c->pipe = new (std::nothrow) HostPipe();
     if (!c->pipe) return ECW_ENOMEM;
@@ -1299,31 +1418,9 @@ extern "C++" bool busy(int device) {
   return sv->ctl && sv->epoch != 0 && __atomic_load_n(&sv->ctl->exited_epoch, __ATOMIC_ACQUIRE) != sv->epoch;
 }
 
-#ifndef ECW_SVC_TRACE
-#define ECW_SVC_TRACE 0  // tools only (tools/variants.py): per-phase latency of served calls, printed at exit
-#endif
-#if ECW_SVC_TRACE
-// host ns: copy in, post -> done seen, copy out; device ticks of the last
-// part: seen -> acquired, -> start, -> computed, -> fenced
-double g_tr[7] = {};
-unsigned long long g_tr_n = 0;
-#endif
-
 void stop_all() {
   std::lock_guard<std::mutex> lk(g_mu);
   for (auto& kv : g_services) kv.second->stop();
-#if ECW_SVC_TRACE
-  if (g_tr_n) {
-    int khz = 100000;
-    (void)hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, 0);
-    const double n = static_cast<double>(g_tr_n), tick_us = 1e3 / khz;
-    std::fprintf(stderr,
-                 "svc trace (%llu calls, us): copy-in %.2f  post->done %.2f  copy-out %.2f | device (last part): seen -> "
-                 "acquired %.2f  -> start %.2f  -> computed %.2f  -> fenced %.2f\n",
-                 g_tr_n, g_tr[0] / n / 1e3, g_tr[1] / n / 1e3, g_tr[2] / n / 1e3, g_tr[3] / n * tick_us,
-                 g_tr[4] / n * tick_us, g_tr[5] / n * tick_us, g_tr[6] / n * tick_us);
-  }
-#endif
 }
 
 Service* service_for(int device) {
@@ -1392,13 +1489,7 @@ extern "C++" int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8
     return st;
   };
   uint8_t* h = sv->stage[slot];
-#if ECW_SVC_TRACE
-  const auto tr0 = std::chrono::steady_clock::now();
-#endif
   for (int j = 0; j < k; ++j) std::memcpy(h + j * cs, data[j], len);
-#if ECW_SVC_TRACE
-  const auto tr1 = std::chrono::steady_clock::now();
-#endif
   SvcSlot& q = sv->ctl->slot[slot];
   // only this thread writes the slot while it holds it
   const SvcSlot want = [&] {
@@ -1427,7 +1518,6 @@ extern "C++" int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8
   }
   const unsigned long long units = (len + kSvcThreads * 4 - 1) / (kSvcThreads * 4);
   const int active = static_cast<int>(std::min<unsigned long long>(units, kSvcParts));
-  const unsigned long long prev_seq = q.seq;
   const unsigned long long seq = (gen << kSvcSeqBits) | (static_cast<unsigned long long>(active) << 32) |
                                  (((q.seq & kSvcReqMask) + 1) & kSvcReqMask);
   __atomic_store_n(&q.seq, seq, __ATOMIC_RELEASE);
@@ -1467,11 +1557,17 @@ extern "C++" int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8
     // to) and a hold keeps the next one from starting: take the launch path
     // now instead of waiting for every hold to end. The service stays on. No
     // kernel polls while the epoch is gone and none starts while mu is held,
-    // so the request is withdrawn (the slot's word restored) before the slot
-    // is given back.
+    // so the request is withdrawn before the slot is given back -- by a NEW
+    // request word with no active part (the parts only note it), never by
+    // restoring the previous word: some parts may have finished this request
+    // and published its word in their `done`, and a later request posted with
+    // that same word again would find them "finished" with this one's
+    // results. Request numbers only ever advance.
     if (sv->holds.load(std::memory_order_acquire) > 0 &&
         __atomic_load_n(&sv->ctl->exited_epoch, __ATOMIC_ACQUIRE) == sv->epoch) {
-      __atomic_store_n(&q.seq, prev_seq, __ATOMIC_RELEASE);
+      const unsigned long long withdrawn =
+          (seq & ~((static_cast<unsigned long long>(0xFF) << 32) | kSvcReqMask)) | (((seq & kSvcReqMask) + 1) & kSvcReqMask);
+      __atomic_store_n(&q.seq, withdrawn, __ATOMIC_RELEASE);
       held_off = true;
       break;
     }
@@ -1491,22 +1587,7 @@ extern "C++" int serve(ecw_codec* c, const uint8_t* const* data, int nsrc, uint8
     release(0);
     return decline();
   }
-#if ECW_SVC_TRACE
-  const auto tr2 = std::chrono::steady_clock::now();
-#endif
   for (int i = 0; i < np; ++i) std::memcpy(parity[i], h + static_cast<size_t>(k + i) * cs, len);
-#if ECW_SVC_TRACE
-  {
-    const auto tr3 = std::chrono::steady_clock::now();
-    auto ns = [](auto d) { return static_cast<double>(std::chrono::duration_cast<std::chrono::nanoseconds>(d).count()); };
-    std::lock_guard<std::mutex> lk(g_mu);
-    g_tr[0] += ns(tr1 - tr0);
-    g_tr[1] += ns(tr2 - tr1);
-    g_tr[2] += ns(tr3 - tr2);
-    for (int i = 0; i < 4; ++i) g_tr[3 + i] += static_cast<double>(q.trace[i + 1] - q.trace[i]);
-    ++g_tr_n;
-  }
-#endif
   sv->n_served.fetch_add(1, std::memory_order_relaxed);
   return release(ECW_OK);
 }

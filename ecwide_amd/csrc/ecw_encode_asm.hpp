@@ -58,11 +58,6 @@
   "v_perm_b32 " A7 ", v32, v35, s53\n\t"
 
 // lo-nibble products at +0, hi-nibble products at +64 of the record
-#if defined(ECW_ASM_ABLATE) && ECW_ASM_ABLATE == 2
-// tuning builds only: every VALU instruction of the math, no LDS lookup (the
-// folds take the addresses)
-#define ECW_DW_READ(A0, A1, A2, A3, A4, A5, A6, A7)
-#else
 #define ECW_DW_READ(A0, A1, A2, A3, A4, A5, A6, A7) \
   "ds_read_b32 " A0 ", " A0 "\n\t"                   \
   "ds_read_b32 " A1 ", " A1 " offset:64\n\t"         \
@@ -72,7 +67,6 @@
   "ds_read_b32 " A5 ", " A5 " offset:64\n\t"         \
   "ds_read_b32 " A6 ", " A6 "\n\t"                   \
   "ds_read_b32 " A7 ", " A7 " offset:64\n\t"
-#endif
 
 #define ECW_DW_FOLD(C0, C1, C2, C3, A0, A1, A2, A3, A4, A5, A6, A7) \
   "v_bitop3_b32 " C0 ", " C0 ", " A0 ", " A1 " bitop3:0x96\n\t"      \
@@ -89,13 +83,6 @@
 
 // One data row from ring slot R0..R3 (s46 = its LDS table record): GF
 // products into the accumulators, XOR into the local parity (XL = 1).
-#ifndef ECW_ASM_PIPE
-#define ECW_ASM_PIPE 1
-#endif
-#ifndef ECW_ASM_EARLY_LOAD
-#define ECW_ASM_EARLY_LOAD 1
-#endif
-#if ECW_ASM_PIPE && (!defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2)
 // Software-pipelined across rows: the row's last lookup set (Y, from R3) is
 // left in flight and folded after the next row's first set has been issued,
 // so the LDS lookups never drain at a row boundary -- not behind the next
@@ -128,35 +115,6 @@
 #define ECW_ROW_YZERO                                                 \
   "v_mov_b32 v49, 0\n\tv_mov_b32 v50, 0\n\tv_mov_b32 v51, 0\n\tv_mov_b32 v52, 0\n\t" \
   "v_mov_b32 v53, 0\n\tv_mov_b32 v54, 0\n\tv_mov_b32 v55, 0\n\tv_mov_b32 v56, 0\n\t"
-#elif !defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2
-#define ECW_ROW_DRAIN
-#define ECW_ROW_YZERO
-#define ECW_ROW_POST
-#define ECW_ROW_PRE(R0, R1, R2, R3, XL)                               \
-  "s_lshr_b32 s47, s46, 8\n\t"                                        \
-  "s_and_b32 s48, s46, 0xff\n\t"                                      \
-  "s_mul_i32 s48, s48, 0x01010101\n\t"                                \
-  "v_mov_b32 v32, s47\n\t"                                            \
-  ECW_ADDR_X(R0) ECW_READ_X                                           \
-  ECW_ADDR_Y(R1) ECW_READ_Y                                           \
-  "s_waitcnt lgkmcnt(8)\n\t"                                          \
-  ECW_FOLD_X("v12", "v13", "v14", "v15")                              \
-  ECW_ADDR_X(R2) ECW_READ_X                                           \
-  "s_waitcnt lgkmcnt(8)\n\t"                                          \
-  ECW_FOLD_Y("v16", "v17", "v18", "v19")                              \
-  ECW_ADDR_Y(R3) ECW_READ_Y                                           \
-  "s_waitcnt lgkmcnt(8)\n\t"                                          \
-  ECW_FOLD_X("v20", "v21", "v22", "v23")                              \
-  ECW_LACC_##XL(R0, R1, R2, R3)                                       \
-  "s_waitcnt lgkmcnt(0)\n\t"                                          \
-  ECW_FOLD_Y("v24", "v25", "v26", "v27")                              \
-  "s_add_u32 s46, s46, 128\n\t"
-#else  // tuning builds only: the memory stream without the GF math
-#define ECW_ROW_DRAIN
-#define ECW_ROW_YZERO
-#define ECW_ROW_POST
-#define ECW_ROW_PRE(R0, R1, R2, R3, XL) ECW_LACC_##XL(R0, R1, R2, R3) "s_add_u32 s46, s46, 128\n\t"
-#endif
 #define ECW_ROW(R0, R1, R2, R3, XL) ECW_ROW_PRE(R0, R1, R2, R3, XL) ECW_ROW_POST
 
 #define ECW_LACC_0(R0, R1, R2, R3)
@@ -304,27 +262,15 @@
   "s_branch 34b\n\t"                                                        \
   "35:\n\t"
 
-#ifndef ECW_ASM_DIAG_NOSTORE
-#define ECW_ASM_GSTORE(V, S) "global_store_dwordx4 v40, " V ", " S ECW_ASM_STMOD "\n\t"
-#else
-#define ECW_ASM_GSTORE(V, S)  // diagnostic builds only: the encode's reads and math without any store
-#endif
-#ifndef ECW_ASM_DIAG_NOLSTORE
-#define ECW_ASM_LSTORE ECW_ASM_GSTORE("v[28:31]", "s[42:43]")
-#else
-#define ECW_ASM_LSTORE  // diagnostic builds only: time the encode without its local-parity stores
-#endif
-#ifndef ECW_ASM_STMOD
 // parity stores: nontemporal (+3 % encode over plain stores, round 1) at system
 // scope (sc0 sc1: +0.4..0.7 % over nt alone on the tiled slab in three
 // processes, +0.5 % block slab; profiles/r02_encode_store_policy_ab.log)
 #define ECW_ASM_STMOD " nt sc0 sc1"
-#endif
-#ifndef ECW_ASM_LDMOD
 // ring loads: nontemporal, every byte is read once (+2 %, measured); nt sc1 /
 // nt sc0 sc1 the same, sc0 sc1 without nt -9 % (profiles/r02_encode_load_policy_ab.log)
 #define ECW_ASM_LDMOD " nt"
-#endif
+#define ECW_ASM_GSTORE(V, S) "global_store_dwordx4 v40, " V ", " S ECW_ASM_STMOD "\n\t"
+#define ECW_ASM_LSTORE ECW_ASM_GSTORE("v[28:31]", "s[42:43]")
 #define ECW_LOAD_A "global_load_dwordx4 v[4:7], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_LOAD_B "global_load_dwordx4 v[8:11], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_ROW_A(XL) ECW_ROW("v4", "v5", "v6", "v7", XL)
@@ -335,11 +281,7 @@
 // goes out as soon as the slot is consumed (between PRE and POST); TAB: after
 // the row, behind the wait for its row-pointer s_load (ECW_LDWAIT_TAB, which
 // drains the LDS lookups too).
-#if ECW_ASM_EARLY_LOAD
 #define ECW_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW_ROW_POST BND
-#else
-#define ECW_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW_ROW_POST BND LOAD NEXT
-#endif
 #define ECW_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
 
 // The whole tile. BND is the boundary code (ECW_BOUNDARY(ZL, MODE) or
@@ -512,10 +454,6 @@
   ECW2_FOLD1(C1, D1, "v62", "v63", "v64", "v65")           \
   ECW2_FOLD1(C2, D2, "v66", "v67", "v68", "v69")           \
   ECW2_FOLD1(C3, D3, "v70", "v71", "v72", "v73")
-#ifndef ECW2_ASM_PIPE
-#define ECW2_ASM_PIPE 1
-#endif
-#if ECW2_ASM_PIPE && ECW_ASM_PIPE && (!defined(ECW_ASM_ABLATE) || ECW_ASM_ABLATE == 2)
 // Pipelined across rows as ECW_ROW_PRE / ECW_ROW_POST above: the row's last
 // lookup set (Y, from R3) is folded after the next row's first set is issued.
 #define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
@@ -546,42 +484,13 @@
   "v_mov_b32 v62, 0\n\tv_mov_b32 v63, 0\n\tv_mov_b32 v64, 0\n\tv_mov_b32 v65, 0\n\t"     \
   "v_mov_b32 v66, 0\n\tv_mov_b32 v67, 0\n\tv_mov_b32 v68, 0\n\tv_mov_b32 v69, 0\n\t"     \
   "v_mov_b32 v70, 0\n\tv_mov_b32 v71, 0\n\tv_mov_b32 v72, 0\n\tv_mov_b32 v73, 0\n\t"
-#else
-#define ECW2_ROW_PRE(R0, R1, R2, R3, XL)                                               \
-  "s_lshr_b32 s47, s46, 8\n\t"                                                         \
-  "s_and_b32 s48, s46, 0xff\n\t"                                                       \
-  "s_andn2_b32 s63, s46, 0xff\n\t"                                                     \
-  "s_mul_i32 s48, s48, 0x01010101\n\t"                                                 \
-  "v_mov_b32 v32, s47\n\t"                                                             \
-  ECW2_ADDR_X(R0) ECW2_READ_X                                                          \
-  ECW2_ADDR_Y(R1) ECW2_READ_Y                                                          \
-  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
-  ECW2_FOLD_X("v12", "v13", "v14", "v15", "v74", "v75", "v76", "v77")                 \
-  ECW2_ADDR_X(R2) ECW2_READ_X                                                          \
-  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
-  ECW2_FOLD_Y("v16", "v17", "v18", "v19", "v78", "v79", "v80", "v81")                 \
-  ECW2_ADDR_Y(R3) ECW2_READ_Y                                                          \
-  "s_waitcnt lgkmcnt(8)\n\t"                                                           \
-  ECW2_FOLD_X("v20", "v21", "v22", "v23", "v82", "v83", "v84", "v85")                 \
-  ECW_LACC_##XL(R0, R1, R2, R3)                                                        \
-  "s_waitcnt lgkmcnt(0)\n\t"                                                           \
-  ECW2_FOLD_Y("v24", "v25", "v26", "v27", "v86", "v87", "v88", "v89")                 \
-  "s_add_u32 s46, s46, 256\n\t"
-#define ECW2_ROW_POST
-#define ECW2_ROW_DRAIN
-#define ECW2_ROW_YZERO
-#endif
 #define ECW2_ROW(R0, R1, R2, R3, XL) ECW2_ROW_PRE(R0, R1, R2, R3, XL) ECW2_ROW_POST
 #define ECW2_ROW_A(XL) ECW2_ROW("v4", "v5", "v6", "v7", XL)
 #define ECW2_ROW_B(XL) ECW2_ROW("v8", "v9", "v10", "v11", XL)
 #define ECW2_ROW_PRE_A(XL) ECW2_ROW_PRE("v4", "v5", "v6", "v7", XL)
 #define ECW2_ROW_PRE_B(XL) ECW2_ROW_PRE("v8", "v9", "v10", "v11", XL)
 // as ECW_STEP_* for the 8-row rows
-#if ECW_ASM_EARLY_LOAD
 #define ECW2_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW2_ROW_POST BND
-#else
-#define ECW2_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW2_ROW_POST BND LOAD NEXT
-#endif
 #define ECW2_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW2_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
 
 #define ECW2_BOUNDARY_PARK                                  \
@@ -874,11 +783,7 @@
 #define ECW4_ROW_B(XL) ECW4_ROW("v8", "v9", "v10", "v11", XL)
 #define ECW4_ROW_PRE_A(XL) ECW4_ROW_PRE("v4", "v5", "v6", "v7", XL)
 #define ECW4_ROW_PRE_B(XL) ECW4_ROW_PRE("v8", "v9", "v10", "v11", XL)
-#if ECW_ASM_EARLY_LOAD
 #define ECW4_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE LOAD NEXT ECW4_ROW_POST BND
-#else
-#define ECW4_STEP_SLAB(PRE, LOAD, NEXT, BND) PRE ECW4_ROW_POST BND LOAD NEXT
-#endif
 #define ECW4_STEP_TAB(PRE, LOAD, NEXT, BND) PRE ECW4_ROW_POST BND ECW_LDWAIT_TAB LOAD NEXT
 
 #define ECW4_BOUNDARY_PARK                                  \

@@ -1,5 +1,6 @@
 // Internal interface between the host codec (ecw_codec.cpp) and the HIP
-// kernels (ecw_kernels.hip). Not part of the C ABI.
+// kernels (ecw_kernels.hip: encode + fill, ecw_xor.hpp: XOR reduce,
+// ecw_service.hip: request service). Not part of the C ABI.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -96,7 +97,7 @@ struct EncodeGeom {
 
 // Launchers return hipSuccess or the launch error (an earlier, unrelated HIP
 // error of the calling thread is cleared first, not reported). The encode
-// launchers run a slab of >= ECW_TICKET_MIN_TILES tiles as one ticket-ordered
+// launchers run a slab of >= kTicketMinTiles tiles as one ticket-ordered
 // launch when `ticket` is given (an 8-byte device counter the caller has
 // zeroed on stream `s` and keeps for this launch alone), else in launch windows.
 hipError_t launch_encode_ptr(const PtrRows& rows, const EncodeGeom& g, const void* d_tbl,
@@ -142,7 +143,7 @@ struct XorGeom {
   uint64_t len, tiles;
   int stripes, n;
 };
-// Set by the XOR launcher (ecw_kernels.hip launch_xor_range): the kernel's
+// Set by the XOR launcher (ecw_xor.hpp launch_xor_range): the kernel's
 // unit is a group of K column tiles (K a template argument of the kernel).
 struct XorSched {
   FastDiv per;            // column groups per stripe
@@ -161,6 +162,19 @@ hipError_t launch_fill_random(uint8_t* dst, uint64_t bstride, uint64_t sstride, 
                               uint64_t offset, uint64_t seed, int s0, int b0, hipStream_t s);
 
 int device_cu_count(int device);
+
+// Process-wide launch schedule (ecwide.h ecw_schedule; -1 = the launcher's
+// own choice). Seeded once from ECW_XOR_SCHED / ECW_WRITE_WINDOW /
+// ECW_XCD_REMAP at first use, then changed only by ecw_set_schedule; the
+// launchers take one copy per launch (ecw_codec.cpp), never the environment.
+struct Schedule {
+  int xor_skew, xor_order, xor_log2p, xor_width;
+  int enc_log2p, enc_width;
+  int xcd_remap;
+};
+Schedule current_schedule();
+// XOR skews compiled into the library (xor_kernel_fixed<N, K>)
+constexpr int kXorSkews[] = {1, 2, 4};
 
 // Stripes one launch may cover when each has `tiles` column tiles: the
 // kernels number tiles in 32 bits, so a launch covers fewer than 2^31 tiles
@@ -222,7 +236,6 @@ struct alignas(64) SvcSlot {
   unsigned long long len, cs;
   unsigned long long serial;  // the codec's unique serial: tables staged in LDS are its tables
   int k, nrows, m, r, groups, local_mode, nw, flags;  // flags: kSvcXorRow
-  unsigned long long trace[8];  // tools only (ECW_SVC_TRACE): phase stamps of the last part
 };
 
 struct SvcCtl {

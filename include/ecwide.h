@@ -205,6 +205,33 @@ int ecw_repair(ecw_codec* codec, const uint8_t* const* blocks, int lost_block, u
  * device the service never ran on. */
 int ecw_service_counters(int device, unsigned long long out[4]);
 
+/* ---- launch schedule (tuning; no reference counterpart) ----------------
+ * Process-wide knobs of HOW the kernels are launched: the tile order and the
+ * write windows. None changes a result byte (tested against
+ * the oracle at every setting), only the order and timing of HBM accesses.
+ * A field of -1 leaves that choice to the library (the default everywhere:
+ * the per-layout choice DESIGN.md §4 measures). The environment variables
+ * ECW_XOR_SCHED="K,ORDER[,LOG2P,W]", ECW_WRITE_WINDOW=off|on|"LOG2P,W" and
+ * ECW_XCD_REMAP=0|1 seed the schedule once, at the first launch or schedule
+ * call; after that only ecw_set_schedule changes it (the environment is never
+ * read per launch). Every launch takes one consistent copy, so the schedule
+ * may be set from any thread; launches already queued keep theirs. */
+typedef struct ecw_schedule {
+  int xor_skew;         /* XOR reduce: column tiles per workgroup, read diagonally: 1, 2 or 4 */
+  int xor_order;        /* XOR reduce: 0 = groups stripe-major, 1 = column-major */
+  int xor_window_log2p; /* XOR reduce write window: period of 2^log2p ticks of the 100 MHz clock, 4..24 */
+  int xor_window_width; /*   stores wait for the first `width` ticks of every period; 0 = no window */
+  int enc_window_log2p; /* encode write window: period, 4..24 */
+  int enc_window_width; /*   width in ticks; 0 = no window */
+  int xcd_remap;        /* per-XCD contiguous tile order of the encode and the XOR: 0 or 1 */
+} ecw_schedule;
+/* Set the schedule (NULL: every field back to -1). A window with only one of
+ * log2p / width set takes the default for the other (2^11 ticks, 64).
+ * ECW_EINVAL, and nothing changed, for a value out of range or a skew the
+ * library was not built with. */
+int ecw_set_schedule(const ecw_schedule* schedule);
+int ecw_get_schedule(ecw_schedule* out);
+
 /* ---- device-memory entry points (asynchronous on `stream`) -------------
  * All pointers are HBM addresses, 16-byte aligned. The pointer arrays
  * themselves are host arrays (copied into the kernel arguments). */

@@ -31,6 +31,15 @@ def E():
     return ecwide_amd
 
 
+@pytest.fixture
+def schedule(E):
+    """The test sets the process's launch schedule (ecw_set_schedule); it is
+    back to the library's own choice (all -1) afterwards."""
+    E.set_schedule()
+    yield
+    E.set_schedule()
+
+
 def make_codec(E, e, local_mode="xor"):
     t = e["code_type"]
     B = e["len"]
@@ -346,8 +355,9 @@ def test_ticket_launches_on_per_thread_streams(E, torch, orc):
     (16, 3, 4, "literal", "blocks"),  # zero L blocks
     (32, 3, 11, "xor", "ptr"),        # device pointer tables
 ])
-def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, layout):
-    """The write window (ecw_kernels.hip set_write_window) only delays the
+def test_write_window_same_bytes(E, torch, orc, schedule, k, m, r, local, layout):
+    """The write window (ecw_kernels.hip set_schedule; ecw_set_schedule's
+    enc_window_*) only delays the
     parity stores: encodes with it forced off, on, and at another period give
     identical parities, equal to the oracle on a column window, and the default
     choice ('auto': whole-block slabs and pointer modes at k >= 64, <= 4 global rows, blocks >= 64 KiB,
@@ -361,10 +371,7 @@ def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, lay
         data = [[src.block(s, j) for j in range(k)] for s in range(S)]
     outs = {}
     for env in ("off", "on", "10,32", None):
-        if env is None:
-            monkeypatch.delenv("ECW_WRITE_WINDOW", raising=False)
-        else:
-            monkeypatch.setenv("ECW_WRITE_WINDOW", env)
+        E.set_schedule(**E.parse_schedule(window=env))
         if layout == "ptr":
             par = [[torch.empty(B, dtype=torch.uint8, device="cuda") for _ in range(np_)] for _ in range(S)]
             E.BlockBatch(c, data, par).encode()
@@ -390,16 +397,13 @@ def test_write_window_same_bytes(E, torch, orc, monkeypatch, k, m, r, local, lay
 
 
 @pytest.mark.parametrize("remap", ["0", "1", None])
-def test_xcd_remap_same_bytes(E, torch, orc, monkeypatch, remap):
-    """The per-XCD tile order (ECW_XCD_REMAP; default on for pointer-table
+def test_xcd_remap_same_bytes(E, torch, orc, schedule, remap):
+    """The per-XCD tile order (ecw_set_schedule's xcd_remap; default on for pointer-table
     encodes, off elsewhere) only permutes which workgroup takes which tile:
     pointer-table encode and repair, and the split slab's encode, give the
     oracle's bytes with it on, off and at the default, with a grid that is and
     one that is not a multiple of 8 workgroups."""
-    if remap is None:
-        monkeypatch.delenv("ECW_XCD_REMAP", raising=False)
-    else:
-        monkeypatch.setenv("ECW_XCD_REMAP", remap)
+    E.set_schedule(**E.parse_schedule(remap=remap))
     k, m, r = 64, 3, 16
     for B, S in ((1 << 20, 32), (3 * 4096 + 64, 5)):  # 8192 tiles; 20 tiles (+ ragged)
         c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
@@ -544,10 +548,11 @@ def test_xor_reduce_ptrs_dev_vs_oracle(E, torch, orc, n, ln, S):
         assert (got[ln:] == 0x5A).all(), s
 
 
-@pytest.mark.parametrize("sched", [None, "1,0", "4,0", "4,1", "1,1", "4,0,11,64", "1,0,10,32", "4,1,12,128"])
-def test_xor_schedules_same_bytes(E, torch, orc, monkeypatch, sched):
-    """Every XOR schedule (ecw_kernels.hip launch_xor_range; ECW_XOR_SCHED =
-    "K,ORDER[,LOG2P,W]": K column tiles per workgroup read diagonally,
+@pytest.mark.parametrize("sched", [None, "1,0", "2,0", "4,0", "4,1", "2,1", "1,1", "4,0,11,64", "2,0,11,64",
+                                   "2,0,10,32", "1,0,10,32", "4,1,12,128", "4,0+r"])
+def test_xor_schedules_same_bytes(E, torch, orc, schedule, sched):
+    """Every XOR schedule (ecw_xor.hpp launch_xor_range; ecw_set_schedule's
+    xor_* fields, written "K,ORDER[,LOG2P,W]": K column tiles per workgroup read diagonally,
     column-major group order, write window; None = the library's choice) gives
     the oracle's bytes through all four source forms (pointer mode, device
     pointer tables, split slab, block slab), with whole groups of K tiles, a
@@ -557,10 +562,8 @@ def test_xor_schedules_same_bytes(E, torch, orc, monkeypatch, sched):
 
     from ecwide_amd._lib import lib
 
-    if sched is None:
-        monkeypatch.delenv("ECW_XOR_SCHED", raising=False)
-    else:
-        monkeypatch.setenv("ECW_XOR_SCHED", sched)
+    base, _, r = (sched or "").partition("+")  # "+r": with the per-XCD group order
+    E.set_schedule(**E.parse_schedule(xor=base or None, remap="1" if r == "r" else None))
     ln, S = 5 * 16384 + 2 * 4096 + 48, 3
     strm = c_void_p(torch.cuda.current_stream().cuda_stream)
     for n in (1, 5, 27, 32):

@@ -333,17 +333,27 @@ def test_service_not_stranded_by_bulk_holds(E, orc):
                 errors.append(("bulk", t))
                 return
 
+    # every small call encodes different data (a rotation of 16
+    # inputs, each against its own oracle output) into zeroed outputs, so a
+    # call handed an earlier request's results -- e.g. by a request word that
+    # aliases a withdrawn one -- fails instead of matching byte for byte
+    sets = [[orc.fill(4096, 650 + i, 0, j) for j in range(11)] for i in range(16)]
+    wants = [ors.encode(d) for d in sets]
+
     def small():
-        data = [orc.fill(4096, 650, 0, j) for j in range(11)]
-        want = ors.encode(data)
         par = [np.zeros(4096, np.uint8) for _ in range(3)]
+        i = 0
         while not stop.is_set():
+            data, want = sets[i % 16], wants[i % 16]
+            for p in par:
+                p[:] = 0
             t0 = time.perf_counter()
             rs.encodeData(data, par)
             lat.append(time.perf_counter() - t0)
             if not all(np.array_equal(a, b) for a, b in zip(par, want)):
-                errors.append(("small",))
+                errors.append(("small", i))
                 return
+            i += 1
 
     th = [threading.Thread(target=bulk, args=(t,)) for t in range(2)] + [threading.Thread(target=small)]
     for x in th:

@@ -193,3 +193,69 @@ def test_chunk_generator_names():
     assert st[0] == "D_7_0" and st[32] == "G_7_0" and st[-1] == "L_7_2"
     rs = chunk_file_names(E.CodingScheme.getRsScheme(4, 2, 64), -1)
     assert rs == ["1_D_0", "2_D_1", "3_D_2", "4_D_3", "5_G_0", "6_G_1"]
+
+
+# ---- launch schedule (ecw_set_schedule): set / get / validation, no launch ----
+def test_schedule_set_get_roundtrip():
+    prev = E.set_schedule()
+    try:
+        assert E.get_schedule() == {f: -1 for f in E.codec.SCHEDULE_FIELDS}
+        E.set_schedule(xor_skew=2, xor_order=1, xor_window_width=32, xcd_remap=1)
+        got = E.get_schedule()
+        # a window with only the width given takes the default period (2^11)
+        assert got == dict(xor_skew=2, xor_order=1, xor_window_log2p=11, xor_window_width=32,
+                           enc_window_log2p=-1, enc_window_width=-1, xcd_remap=1)
+        E.set_schedule(enc_window_log2p=10)  # only the period: the default width (64)
+        assert (E.get_schedule()["enc_window_log2p"], E.get_schedule()["enc_window_width"]) == (10, 64)
+        assert _lib.lib.ecw_set_schedule(None) == 0
+        assert E.get_schedule() == {f: -1 for f in E.codec.SCHEDULE_FIELDS}
+    finally:
+        E.set_schedule(**{k: v for k, v in prev.items() if v != -1})
+
+
+@pytest.mark.parametrize("bad", [dict(xor_skew=3), dict(xor_skew=8), dict(xor_skew=0), dict(xor_order=2),
+                                 dict(xor_window_log2p=3), dict(enc_window_log2p=25), dict(xcd_remap=2),
+                                 dict(enc_window_width=-5)])
+def test_schedule_rejects_out_of_range(bad):
+    """a skew the library was not built with (or any value out of
+    range) is refused with ECW_EINVAL and changes nothing -- never silently
+    run as K = 1."""
+    E.set_schedule(xor_skew=4)
+    try:
+        with pytest.raises(E.EcwError):
+            E.set_schedule(**bad)
+        assert E.get_schedule()["xor_skew"] == 4
+    finally:
+        E.set_schedule()
+
+
+def test_parse_schedule_strings():
+    assert E.parse_schedule(xor="2,1") == dict(xor_skew=2, xor_order=1, xor_window_width=0)
+    assert E.parse_schedule(xor="4,0,10,32") == dict(xor_skew=4, xor_order=0, xor_window_log2p=10,
+                                                     xor_window_width=32)
+    assert E.parse_schedule(window="off", remap="1") == dict(enc_window_width=0, xcd_remap=1)
+    assert E.parse_schedule(window="12,128") == dict(enc_window_log2p=12, enc_window_width=128)
+    assert E.parse_schedule(xor="auto", window=None) == {}
+
+
+def test_schedule_seeded_from_environment_once():
+    """The environment seeds the schedule once (a fresh process); malformed
+    values are reported and ignored."""
+    import subprocess
+    import sys
+
+    code = ("import ecwide_amd as E, os; print(E.get_schedule()); os.environ['ECW_XCD_REMAP'] = '0'; "
+            "print(E.get_schedule())")
+    env = dict(os.environ, ECW_XOR_SCHED="2,1,10,32", ECW_WRITE_WINDOW="off", ECW_XCD_REMAP="1")
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    first, second = [eval(x) for x in out.stdout.strip().splitlines()]
+    assert first == dict(xor_skew=2, xor_order=1, xor_window_log2p=10, xor_window_width=32,
+                         enc_window_log2p=-1, enc_window_width=0, xcd_remap=1)
+    assert second == first  # read once: a later setenv changes nothing
+    env = dict(os.environ, ECW_XOR_SCHED="3,0", ECW_WRITE_WINDOW="bogus")
+    out = subprocess.run([sys.executable, "-c", "import ecwide_amd as E; print(E.get_schedule())"], env=env,
+                         capture_output=True, text=True, check=True,
+                         cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    assert eval(out.stdout.strip()) == {f: -1 for f in E.codec.SCHEDULE_FIELDS}
+    assert "ECW_XOR_SCHED" in out.stderr and "ECW_WRITE_WINDOW" in out.stderr

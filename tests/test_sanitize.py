@@ -16,10 +16,12 @@ OUT = os.path.join(REPO, "build", "asan")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 SOURCES = [os.path.join(REPO, p) for p in (
     "tests/csrc/asan_host.cpp", "ecwide_amd/csrc/ecw_codec.cpp", "ecwide_amd/csrc/ecw_kernels.hip",
-    "ecwide_amd/csrc/ecw_isal_shim.cpp", "ecwide_amd/csrc/jni/ecw_jni.cpp", "tests/jni/jvm_double.cpp")]
+    "ecwide_amd/csrc/ecw_xor_ptr.hip", "ecwide_amd/csrc/ecw_xor_slab.hip",
+    "ecwide_amd/csrc/ecw_service.hip", "ecwide_amd/csrc/ecw_isal_shim.cpp", "ecwide_amd/csrc/jni/ecw_jni.cpp", "tests/jni/jvm_double.cpp")]
 DEPS = SOURCES + [os.path.join(REPO, p) for p in (
     "include/ecwide.h", "ecwide_amd/csrc/ecw_gf.hpp", "ecwide_amd/csrc/ecw_internal.hpp",
-    "ecwide_amd/csrc/ecw_encode_asm.hpp", "tests/jni/jni.h")]
+    "ecwide_amd/csrc/ecw_tuning.hpp", "ecwide_amd/csrc/ecw_device.hpp", "ecwide_amd/csrc/ecw_xor.hpp", "ecwide_amd/csrc/ecw_encode_asm.hpp",
+    "tests/jni/jni.h")]
 FLAGS = ["--offload-arch=gfx950", "-O1", "-g", "-std=c++17", "-fno-omit-frame-pointer",
          "-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
          "-Xarch_host", "-fno-sanitize-recover=undefined",

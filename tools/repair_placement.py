@@ -1,0 +1,187 @@
+#!/usr/bin/env python3
+"""Placement robustness of the tiled slab's CL repair.
+
+Several identical tiled slabs (the bench's headline layout: 8 KiB column
+pieces, CL(128, 27, 3), 64 MiB blocks) and one split slab (whole blocks: the
+reference layout, as a same-process yardstick) are allocated side by side in
+ONE process; where each allocation lands physically sets its rate (DESIGN.md
+§5). Every XOR schedule (ecw_set_schedule: K column tiles per workgroup read
+diagonally, group order, write window) is timed on every slab in interleaved
+rounds, and a schedule is judged by its WORST slab, not its median: the bench
+line gets one allocation, and a schedule that is fast on a good placement but
+slow on a bad one is what the driver's box sees.
+
+  python tools/repair_placement.py [--slabs 5] [--stripes 4] [--rounds 4] [--scheds auto 1,0 2,0,11,64 ...]
+  rocprofv3 --pmc ... -- python3 tools/repair_placement.py --pmc-reps 3 ...   (fixed dispatch order)
+  python tools/repair_placement.py --summarize <counter_collection.csv> [same --slabs/--scheds/--pmc-reps]
+
+Schedules are "K,ORDER[,LOG2P,W]" (ecwide_amd.parse_schedule; no window unless
+given) or "auto" (the library's own choice).
+"""
+import argparse
+import csv
+import os
+import statistics
+import sys
+from collections import defaultdict
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+SCHEDS = ["auto", "1,0", "2,0", "4,0", "1,0,11,64", "2,0,11,64", "4,0,11,64", "2,0,10,32", "4,0,10,32", "2,1,11,64"]
+
+
+def legs(a):
+    """(slab index, schedule) in the order the PMC mode dispatches them."""
+    names = [f"T{i}" for i in range(a.slabs)] + (["S"] if a.split else [])
+    return [(n, sc) for n in names for sc in a.scheds]
+
+
+def run(a):
+    import torch
+
+    import ecwide_amd as E
+
+    k, m, r, B, S = a.k, a.m, a.r, a.mib << 20, a.stripes
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slabs = {}
+    order = [f"T{i}" for i in range(a.slabs)]
+    if a.split:
+        order.insert(min(a.split_at, len(order)), "S")
+    for n in order:  # allocated in this order, side by side
+        sl = E.StripeSlab(c, stripes=S, block_bytes=B, layout="split" if n == "S" else "tiled")
+        sl.fill_random(seed=a.seed)
+        slabs[n] = sl
+    out = torch.empty(S * B, dtype=torch.uint8, device="cuda")
+    for n, sl in slabs.items():
+        sl.encode()
+    torch.cuda.synchronize()
+    print("allocation order " + " ".join(f"{n}@0x{slabs[n].buf.data_ptr():x}" for n in order), flush=True)
+    rbytes = slabs[order[0]].repair_bytes(0)
+    ebytes = slabs[order[0]].encode_bytes()
+    names = list(slabs)
+
+    def timed(fn, iters):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        return e0.elapsed_time(e1) * 1e-3 / iters
+
+    def set_sched(sc):
+        E.set_schedule(**E.parse_schedule(xor=None if sc == "auto" else sc))
+
+    # every (slab, schedule) once, checked against D0
+    for n in names:
+        for sc in a.scheds:
+            set_sched(sc)
+            out.fill_(0)
+            slabs[n].repair(0, out)
+            torch.cuda.synchronize()
+            for s in (0, S - 1):
+                if not torch.equal(out[s * B:(s + 1) * B], slabs[n].block(s, 0)):
+                    raise SystemExit(f"slab {n} schedule {sc}: repair != D0 (stripe {s})")
+    print(f"every (slab, schedule) repair == D0 ({len(names)} slabs x {len(a.scheds)} schedules)", flush=True)
+    if a.pmc_reps:
+        # fixed order for the counter passes: legs() order, pmc_reps dispatches each
+        for n, sc in legs(a):
+            set_sched(sc)
+            for _ in range(a.pmc_reps):
+                slabs[n].repair(0, out)
+            torch.cuda.synchronize()
+        E.set_schedule()
+        for n in names:  # then each slab's encode (its placement's rate for the streaming mix)
+            for _ in range(a.pmc_reps):
+                slabs[n].encode()
+        torch.cuda.synchronize()
+        print("pmc order done", flush=True)
+        return
+    rep = defaultdict(list)
+    enc = defaultdict(list)
+    combos = [(n, sc) for n in names for sc in a.scheds]
+    for rd in range(a.rounds):
+        rot = combos[(rd * 7) % len(combos):] + combos[:(rd * 7) % len(combos)]
+        for n, sc in rot:
+            set_sched(sc)
+            rep[(n, sc)].append(rbytes / timed(lambda: slabs[n].repair(0, out), a.iters) / 1e9)
+        E.set_schedule()
+        for n in names:
+            enc[n].append(ebytes / timed(slabs[n].encode, 2) / 1e9)
+        print(f"round {rd + 1}/{a.rounds} done", flush=True)
+    E.set_schedule()
+    med = {key: statistics.median(v) for key, v in rep.items()}
+    print(f"\nCL(k={k}, r={r}, m={m}) B={a.mib} MiB x {S} stripes per slab; D0 repair GB/s, median of {a.rounds} "
+          f"interleaved rounds x {a.iters} launches; T* = tiled slabs (8 KiB pieces), S = split slab")
+    print("slab  encode  " + " ".join(f"{sc:>11s}" for sc in a.scheds))
+    for n in names:
+        print(f"{n:4s} {statistics.median(enc[n]):7.1f} " + " ".join(f"{med[(n, sc)]:11.1f}" for sc in a.scheds))
+    tiled = [n for n in names if n.startswith("T")]
+    print("\nper schedule over the tiled slabs: worst / median / best (GB/s), worst vs the split slab's default")
+    split_auto = med.get(("S", "auto"))
+    rank = []
+    for sc in a.scheds:
+        v = sorted(med[(n, sc)] for n in tiled)
+        rel = f"  worst/split_auto {v[0] / split_auto:.4f}" if split_auto else ""
+        print(f"  {sc:11s} {v[0]:7.1f} {statistics.median(v):7.1f} {v[-1]:7.1f}{rel}")
+        rank.append((v[0], sc))
+    best = max(rank)
+    print(f"best by worst tiled slab: {best[1]} ({best[0]:.1f} GB/s)")
+    if split_auto:
+        sv = [med[("S", sc)] for sc in a.scheds]
+        print("split slab: " + " ".join(f"{sc}={x:.1f}" for sc, x in zip(a.scheds, sv)))
+
+
+def summarize(a):
+    per = defaultdict(lambda: defaultdict(float))
+    eper = defaultdict(lambda: defaultdict(float))
+    for path in a.summarize:
+        with open(path) as f:
+            for row in csv.DictReader(f):
+                name = row.get("Kernel_Name", "")
+                tgt = per if "xor_kernel_fixed" in name else eper if "encode_kernel_asm" in name else None
+                if tgt is None:
+                    continue
+                tgt[int(row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
+    ids = sorted(per)
+    L = legs(a)
+    # the correctness pass dispatches every leg once first
+    ids = ids[len(L):]
+    if len(ids) != len(L) * a.pmc_reps:
+        print(f"warning: {len(ids)} timed xor dispatches, expected {len(L) * a.pmc_reps}")
+    B, S = a.mib << 20, a.stripes
+    for i, (n, sc) in enumerate(L):
+        grp = ids[i * a.pmc_reps:(i + 1) * a.pmc_reps]
+        if not grp:
+            break
+        cs = sorted({c for d in grp for c in per[d]})
+        avg = {c: sum(per[d][c] for d in grp) / len(grp) for c in cs}
+        extra = ""
+        if avg.get("TCC_EA0_RDREQ_sum") and "TCC_EA0_RDREQ_LEVEL_sum" in avg:
+            extra += f" read level/req {avg['TCC_EA0_RDREQ_LEVEL_sum'] / avg['TCC_EA0_RDREQ_sum']:.1f}"
+        if "FETCH_SIZE" in avg:
+            extra += f" read/alg {avg['FETCH_SIZE'] * 1024 * 2 / (S * a.r * B):.5f}"
+        print(f"{n:3s} {sc:11s} " + " ".join(f"{c}={v:.4g}" for c, v in avg.items()) + extra)
+    eids = sorted(eper)
+    print(f"encode dispatches: {len(eids)} (the last {a.pmc_reps * 2} per slab, slab order)")
+
+
+if __name__ == "__main__":
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--k", type=int, default=128)
+    ap.add_argument("--m", type=int, default=3)
+    ap.add_argument("--r", type=int, default=27)
+    ap.add_argument("--mib", type=int, default=64)
+    ap.add_argument("--stripes", type=int, default=4)
+    ap.add_argument("--slabs", type=int, default=5)
+    ap.add_argument("--split", type=int, default=1, help="1: also a split slab (the same-process yardstick)")
+    ap.add_argument("--split-at", type=int, default=2, help="its position in the allocation order")
+    ap.add_argument("--scheds", nargs="+", default=SCHEDS)
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=4)
+    ap.add_argument("--seed", type=int, default=103)
+    ap.add_argument("--pmc-reps", type=int, default=0)
+    ap.add_argument("--summarize", nargs="*")
+    a = ap.parse_args()
+    summarize(a) if a.summarize else run(a)

@@ -3,8 +3,13 @@
 
   python tools/variants.py name=-DECW_PREFETCH_ENC=8 other=-DECW_ABLATE=1,-DECW_GRID_PER_CU=4 ...
 
-Each spec is name=comma-separated extra flags. Used with tools/kbench.py on
-the GPU box (the .so files travel with the snapshot; build/ is git-ignored).
+Each spec is name=comma-separated extra flags: overrides of the compile-time
+tunables in ecwide_amd/csrc/ecw_tuning.hpp. (Run-time launch choices -- tile
+order, write windows, XOR skew -- need no variant: ecw_set_schedule.) The
+round 1-4 diagnostic ablations (math-free, store-free, no-staging builds)
+were retired from the product source in round 5; build them from commit
+90a4d53 (`git worktree add`). Used with tools/kbench.py on the GPU box (the
+.so files travel with the snapshot; build/ is git-ignored).
 """
 import os
 import subprocess
@@ -26,14 +31,16 @@ def one(spec):
     name, _, flags = spec.partition("=")
     extra = [f for f in flags.split(",") if f]
     out = os.path.join(OUT, name + ".so")
-    cmd = [b.HIPCC, *b.FLAGS, *extra, *b.SOURCES, "-o", out]
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    return name, r.returncode, r.stderr[-2000:]
+    try:
+        b.compile_lib(out, extra, obj_dir=os.path.join(OUT, "obj_" + name))
+        return name, 0, ""
+    except subprocess.CalledProcessError as e:
+        return name, e.returncode, str(e)
 
 
 if __name__ == "__main__":
     os.makedirs(OUT, exist_ok=True)
-    with ThreadPoolExecutor(6) as ex:
+    with ThreadPoolExecutor(2) as ex:  # each build compiles its translation units in parallel
         for name, rc, err in ex.map(one, sys.argv[1:]):
             print(f"{name}: {'ok' if rc == 0 else 'FAILED'}")
             if rc:
