@@ -308,73 +308,101 @@ def host_cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_baseline(args, k, m, r, B):
-    """The reference's CPU path restated (oracle, test infrastructure): ECWide-C
-    encodeData = ec_encode_data with the AVX2 4-bit-split dot products
-    (global rows) + one pass per local group, then decodeData of D0 (XOR of
-    the r survivors), on ONE whole stripe of the bench workload (k blocks of
-    B bytes), single thread (ECWide-C's one ComputeWorker) and the box's
-    per-GPU share of cores."""
+def cpu_stripe(args, k, m, r, B, threads_list, seconds, literal=False, repair=True, seed=None):
+    """One whole stripe of CL(k, r, m) B-byte blocks through the reference's CPU
+    flow, restated (oracle: test infrastructure, never the product): ECWide-C
+    encodeData = ec_encode_data with the AVX2 4-bit-split dot products (global
+    rows) + one pass per local group (NativeCodec.cc:137-219), then (repair)
+    decodeData of D0 = ec_encode_data of the r survivors with the all-ones
+    table (NativeCodec.cc:237-248), both split by byte range over `threads`
+    threads. GB/s (algorithmic bytes: inputs + outputs) per thread count, each
+    timed for about seconds / len(threads_list) (at least one whole stripe)."""
     import ctypes
 
     import numpy as np
 
     import oracle
-    from ecwide_amd.shard import host_threads
 
     orc = oracle.Oracle()
     oc = orc.codec("C", k, m, r, B)
-    rng = np.random.default_rng(args.seed)
+    rng = np.random.default_rng(args.seed if seed is None else seed)
     data = [np.frombuffer(rng.bytes(B), np.uint8) for _ in range(k)]
     par = [np.zeros(B, np.uint8) for _ in range(oc.parity_num)]
     u8p = ctypes.POINTER(ctypes.c_uint8)
-    dp = (u8p * k)(*[d.ctypes.data_as(u8p) for d in data])
-    pp = (u8p * len(par))(*[p.ctypes.data_as(u8p) for p in par])
-    per_stripe = (k + oc.parity_num + r + 1) * B
-    ones = orc.init_tables(r, 1, np.ones(r, np.uint8))
+    dp = (u8p * k)(*[x.ctypes.data_as(u8p) for x in data])
+    pp = (u8p * len(par))(*[x.ctypes.data_as(u8p) for x in par])
+    nsrc = min(r, k)
+    per_stripe = (k + oc.parity_num + ((nsrc + 1) if repair else 0)) * B
+    ones = orc.init_tables(nsrc, 1, np.ones(nsrc, np.uint8))
     rep = np.zeros(B, np.uint8)
     rp = (u8p * 1)(rep.ctypes.data_as(u8p))
-    srcs = data[1:r] + [par[m]]
-    sp = (u8p * r)(*[s.ctypes.data_as(u8p) for s in srcs])
+    srcs = data[1:nsrc] + [par[m]]
+    sp = (u8p * nsrc)(*[x.ctypes.data_as(u8p) for x in srcs])
 
     def run(threads):
-        oc.encode_into(dp, pp, B, literal=False, threads=threads)
-        # decodeData: ec_encode_data with the all-ones table (NativeCodec.cc:248)
-        orc.L.orc_encode_data_avx2(B, r, 1, ones.ctypes.data_as(u8p), sp, rp)
+        oc.encode_into(dp, pp, B, literal=literal, threads=threads)
+        if repair:
+            orc.L.orc_encode_data_avx2_mt(B, nsrc, 1, ones.ctypes.data_as(u8p), sp, rp, threads)
 
+    run(max(threads_list))  # warm: fault in the output pages outside the timing
     res = {}
-    allc = host_threads()
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except AttributeError:
-        affinity = os.cpu_count()
-    run(allc)  # warm: fault in the output pages outside the timing
-    for threads in sorted({1, allc}):
+    for threads in threads_list:
         n, t0 = 0, time.perf_counter()
         while True:
             run(threads)
             n += 1
             el = time.perf_counter() - t0
-            if el > args.cpu_seconds / 2 or n >= 50:
+            if el > seconds / len(threads_list) or n >= 50:
                 break
-        assert np.array_equal(rep, data[0]), "CPU baseline repair mismatch"
-        res[threads] = n * per_stripe / el / 1e9
+        res[threads] = round(n * per_stripe / el / 1e9, 3)
+    ok = True
+    if repair and not literal:
+        ok = bool(np.array_equal(rep, data[0]))
+    return res, ok
+
+
+def cpu_meta(orc=None) -> dict:
+    from ecwide_amd.shard import host_threads
+
+    import oracle
+
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = os.cpu_count()
+    return {"cores_all": host_threads(), "affinity_cores": affinity, "nproc": os.cpu_count(),
+            "cap": 16, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "host_cpu": host_cpu_model(),
+            "avx2": (orc or oracle.Oracle()).have_avx2()}
+
+
+def cpu_baseline(args, k, m, r, B):
+    """The headline workload's CPU baseline (rank 0, N=1): one whole stripe,
+    1 thread (ECWide-C's one ComputeWorker thread) as `value`, and the thread
+    scaling 1 -> 2 -> 4 -> 8 -> the box's per-GPU CPU share (16: the pool's
+    limit for one GPU's job, OMP_NUM_THREADS there) as `value_all_cores`."""
+    from ecwide_amd.shard import host_threads
+
+    allc = host_threads()
+    tl = sorted({t for t in (1, 2, 4, 8) if t < allc} | {allc})
+    res, ok = cpu_stripe(args, k, m, r, B, tl, args.cpu_seconds)
+    if not ok:
+        raise SystemExit("CPU baseline repair mismatch")
+    per_thread = {t: round(v / t, 3) for t, v in res.items()}
     return {
-        "value": round(res[1], 3),
+        "value": res[1],
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
         "sample": (f"1 whole stripe of the workload, CL(k={k},r={r},m={m}) B={B >> 20} MiB: ECWide-C encodeData "
                    f"flow (AVX2 nibble-pshufb port of ISA-L's gf_Nvect_dot_prod_avx2, global + per-group passes) "
                    f"+ decodeData of D0; 1 thread = ECWide-C's one ComputeWorker thread"),
-        "value_all_cores": round(res[allc], 3),
-        "cores_all": allc,  # threads the all-cores run used: min(affinity_cores, OMP_NUM_THREADS, cap)
-        "affinity_cores": affinity,
-        "nproc": os.cpu_count(),
-        "cap": 16,  # host_threads(): the GPU box's per-GPU CPU share (OMP_NUM_THREADS=16 there)
-        "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
-        "host_cpu": host_cpu_model(),
-        "avx2": orc.have_avx2(),
+        "value_all_cores": res[allc],
+        "thread_scaling_GBps": {str(t): v for t, v in res.items()},
+        "per_thread_GBps": {str(t): v for t, v in per_thread.items()},
+        "all_cores_note": (f"{allc} threads = this job's CPU share on the GPU box (the pool gives one GPU's job 16 of "
+                           f"the host's CPUs and caps worker pools there); the host has more cores, which other "
+                           f"jobs use"),
+        **cpu_meta(),
     }
 
 
@@ -498,35 +526,51 @@ def other_layouts(args, E, codec, slab, S, B, out, enc_bytes, rep_bytes, dev) ->
 PCIE_GEN5_X16_GBPS = 63.0  # per direction: 32 GT/s x 16 lanes x 128/130 / 8
 
 
-def host_resident_leg(args, dev: int, iters: int) -> dict:
-    """PCIe-inclusive rate: one stripe's blocks live in pinned host memory;
-    ecw_encode / ecw_repair pipeline them through HBM with hipMemcpyAsync in
-    and out (8 MiB column slices, 3 HBM slots, H2D / kernel / D2H on three
-    streams). Reported beside `value`, never as it."""
+def host_resident_leg(args, d, iters: int) -> dict:
+    """PCIe-inclusive rate on EVERY rank at once: each rank's own stripe
+    (stripe id = rank) lives in pinned host memory on its GPU's NUMA node
+    (ecwide_amd.PinnedHost = ecw_host_alloc: pages preferred on the node of
+    the GPU's PCIe root, faulted in, registered); ecw_encode / ecw_repair
+    pipeline it through HBM with hipMemcpyAsync in and out (8 MiB column
+    slices, 3 HBM slots, H2D / kernel / D2H on three streams). All ranks run
+    between two barriers; the aggregate is every rank's bytes over the
+    slowest rank's time, so at N = 8 it is what the node's eight PCIe links
+    and its DRAM deliver together. Reported beside `value`,
+    never as it. `d` None: one rank (the --host-resident mode)."""
     import numpy as np
     import torch
 
     import ecwide_amd as E
 
+    world, rank, dev = (1, 0, 0) if d is None else (d.world, d.rank, d.dev)
+    barrier = (lambda: None) if d is None else d.barrier
     k, m, r = args.k, args.m, args.r
     B = int((args.block_mib or 64.0) * (1 << 20))
     codec = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, device=dev)
     nblk = k + codec.parityNum
-    hb = torch.empty(nblk * B, dtype=torch.uint8, pin_memory=not args.pageable)
+    t0 = time.perf_counter()
+    host = None
+    if args.pageable:
+        hb, node = np.zeros((nblk + 1) * B, np.uint8), -1
+    else:
+        host = E.PinnedHost((nblk + 1) * B, dev)
+        hb, node = host.array, host.numa_node
+    alloc_s = time.perf_counter() - t0
     slab = E.StripeSlab(codec, stripes=1, block_bytes=B, device=dev)
-    slab.fill_random(seed=args.seed)
+    slab.fill_random(seed=args.seed, s0=rank)
     for j in range(k):
-        hb[j * B:(j + 1) * B].copy_(slab.block(0, j))
+        torch.from_numpy(hb[j * B:(j + 1) * B]).copy_(slab.block(0, j))
     slab.encode()  # the expected parities, from the device-resident path
     want = [p.cpu().numpy() for p in slab.parity(0)]
     del slab
     torch.cuda.synchronize()
-    views = [hb[i * B:(i + 1) * B].numpy() for i in range(nblk)]
-    out = torch.empty(B, dtype=torch.uint8, pin_memory=not args.pageable).numpy()
+    views = [hb[i * B:(i + 1) * B] for i in range(nblk)]
+    out = hb[nblk * B:(nblk + 1) * B]
     nsrc = len(codec.repairSources(0))
     enc_b, rep_b = nblk * B, (nsrc + 1) * B
     codec.encodeData(views[:k], views[k:])  # warm
     codec.repairBlock(views, 0, out)
+    barrier()
     t0 = time.perf_counter()
     for _ in range(iters):
         codec.encodeData(views[:k], views[k:])
@@ -534,23 +578,43 @@ def host_resident_leg(args, dev: int, iters: int) -> dict:
     for _ in range(iters):
         codec.repairBlock(views, 0, out)
     t2 = time.perf_counter()
+    barrier()
+    el = time.perf_counter() - t0
     ok = np.array_equal(out, views[0]) and all(np.array_equal(a, b) for a, b in zip(views[k:], want))
     h2d = iters * (k * B + nsrc * B) / (t2 - t0) / 1e9  # bytes the pipeline moved host -> device per second
+    own = iters * (enc_b + rep_b) / (t2 - t0) / 1e9
+    if host is not None:
+        host.free()
+    gather = (lambda x: [x]) if d is None else d.gather
+    reduce = (lambda x, op: x) if d is None else d.reduce
+    el_max = reduce(el, "max")
+    all_ok = reduce(1.0 if ok else 0.0, "min") > 0.5
+    rank_gbps, rank_h2d = gather(own), gather(h2d)
+    rank_node = [int(x) for x in gather(float(node))]
+    rank_dev_node = [int(x) for x in gather(float(E._lib.lib.ecw_device_numa_node(dev)))]
     return {
-        "GBps": round(iters * (enc_b + rep_b) / (t2 - t0) / 1e9, 2),
+        "GBps": round(world * iters * (enc_b + rep_b) / el_max / 1e9, 2),
+        "scope": ("all ranks at once, each its own stripe in pinned host memory on its GPU's NUMA node; aggregate "
+                  "= every rank's bytes / the slowest rank's time between barriers") if world > 1 else "one rank",
         "encode_GBps": round(iters * enc_b / (t1 - t0) / 1e9, 2),
         "repair_GBps": round(iters * rep_b / (t2 - t1) / 1e9, 2),
-        "pcie_bytes_per_step": (k + codec.parityNum) * B + (nsrc + 1) * B,
+        "pcie_bytes_per_step": enc_b + rep_b,
         "h2d_GBps": round(h2d, 2),
         "frac_of_pcie_gen5_x16": round(h2d / PCIE_GEN5_X16_GBPS, 4),
-        "iters": iters, "verified": bool(ok),
-        "host_blocks": "pageable" if args.pageable else "pinned",
-        "config": f"CL(k={k}, r={r}, m={m}) one stripe of {B >> 20} MiB blocks in host memory: encodeData + "
+        "rank_GBps": [round(x, 2) for x in rank_gbps],
+        "rank_h2d_GBps": [round(x, 2) for x in rank_h2d],
+        "rank_numa_node": rank_node,
+        "rank_gpu_numa_node": rank_dev_node,
+        "numa_local": all(a == b for a, b in zip(rank_node, rank_dev_node)) if not args.pageable else None,
+        "alloc_s": round(alloc_s, 2),
+        "iters": iters, "verified": bool(all_ok),
+        "host_blocks": "pageable" if args.pageable else "pinned, NUMA-local (ecw_host_alloc)",
+        "config": f"CL(k={k}, r={r}, m={m}) one stripe of {B >> 20} MiB blocks per rank in host memory: encodeData + "
                   f"repair of D0; 8 MiB column slices, 3 HBM slots, H2D / kernel / D2H on three streams",
     }
 
 
-def chunkgen_leg(args) -> dict:
+def chunkgen_leg(args, cpu_seconds: float = 0.0) -> dict:
     """ECWide-C's ChunkGenerator replay (BASELINE configs[0]; the default
     ECWide-C/config/scheme.ini: CL k=32, groupDataNum=11, m=3, 64 MiB chunks):
     source blocks in pinned host memory (BufferUnit's direct ByteBuffers),
@@ -589,6 +653,16 @@ def chunkgen_leg(args) -> dict:
         paths = gen.generate_chunks(0)
         wms = (time.perf_counter() - t0) * 1e3
         best = min(ms)
+        cpu = None
+        if cpu_seconds > 0:
+            # the reference's own configs[0] timing on this host: encodeChunks on the CPU, i.e. encodeData of
+            # the same 64 MiB chunks, literal mode, no repair (ChunkGenerator.java:126-131), one thread
+            res, _ = cpu_stripe(args, scheme.k, scheme.globalParityNum, scheme.groupDataNum, B, [1], cpu_seconds,
+                                literal=True, repair=False, seed=args.seed)
+            cpu = {"encodeChunks_GBps": res[1], "encodeChunks_ms": round(nb * B / (res[1] * 1e9) * 1e3, 1),
+                   "cores": 1, "kind": "port",
+                   "sample": "encodeData of one stripe of the default scheme.ini's 64 MiB chunks (literal L), "
+                             "ECWide-C's one ComputeWorker thread"}
         return {
             "config": "ChunkGenerator replay, default scheme.ini: CL(k=32, r=11, m=3), 64 MiB chunks, zero L blocks "
                       "(the reference's bytes), pinned source buffers",
@@ -596,6 +670,7 @@ def chunkgen_leg(args) -> dict:
             "encodeChunks_GBps": round(nb * B / (best * 1e-3) / 1e9, 2),
             "generateChunks_ms": round(wms, 1), "chunk_files": len(paths),
             "generateChunks_GBps": round(nb * B / (wms * 1e-3) / 1e9, 2), "verified": bool(ok),
+            "cpu_baseline": cpu,
         }
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
@@ -606,7 +681,7 @@ def host_resident(args):
     import torch
 
     torch.cuda.set_device(0)
-    leg = host_resident_leg(args, 0, max(1, args.steps // 4))
+    leg = host_resident_leg(args, None, max(1, args.steps // 4))
     line = {"metric": ("host-resident encode + single-block-repair GB/s "
                        + ("(pageable host blocks, e.g. Java direct ByteBuffers)" if args.pageable
                           else "(pinned host blocks, hipMemcpyAsync in/out)")),
@@ -824,7 +899,19 @@ def dry_run(args, d: Dist):
             shapes[name] = {"stripes_per_gpu": ps["share"]["stripes"], "stripes_total": ps["stripes_total"],
                             "block_bytes": ps["block_bytes_full"],
                             "rank_ms_per_step": [round(x / args.shape_steps * 1e3, 4) for x in d.gather(el)]}
-    d.barrier()  # the rank-0-only host legs start after every rank's timed legs
+    d.barrier()  # the host legs start after every rank's timed legs
+    host = None
+    if args.host_iters > 0:
+        # the per-rank host-resident leg's orchestration: every rank between two
+        # barriers, the same gathers as host_resident_leg (no GPU: no pinning)
+        d.barrier()
+        t0 = time.perf_counter()
+        time.sleep(0.01 * (1 + d.rank))
+        d.barrier()
+        hel = d.reduce(time.perf_counter() - t0, "max")
+        host = {"el_max": hel, "rank_GBps": d.gather(0.0), "rank_h2d_GBps": d.gather(0.0),
+                "rank_numa_node": [int(x) for x in d.gather(-1.0)],
+                "rank_gpu_numa_node": [int(x) for x in d.gather(-1.0)]}
     if d.rank == 0:
         print(json.dumps({"dry_run": True, "n_gpus": d.world, "scaling": "strong" if pl["strong"] else "weak",
                           "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
@@ -832,7 +919,7 @@ def dry_run(args, d: Dist):
                           "rank_ms_per_step": [round(x / steps * 1e3, 4) for x in per_rank],
                           "roofline": {"rank_launch_ms": [round(x * 1e3 / steps, 4) for x in per_rank]},
                           "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
-                          "configs4": c4, **shapes,
+                          "configs4": c4, **shapes, "host_resident": host,
                           "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
                                      for a, b, c, o in zip(*shares)]}), flush=True)
     d.close()
@@ -999,6 +1086,20 @@ def shape_leg(args, d: Dist, E, leg_def) -> dict:
     return res
 
 
+def shape_cpu_baseline(args, leg_def) -> dict:
+    """A SHAPE_LEGS entry's CPU baseline: one whole stripe of that shape through
+    the same encodeData + decodeData flow as the headline's, 1 thread (and the
+    box's per-GPU share)."""
+    from ecwide_amd.shard import host_threads
+
+    name, desc, k, m, r, mib, stripes, seed = leg_def
+    allc = host_threads()
+    res, ok = cpu_stripe(args, k, m, r, int(mib) << 20, sorted({1, allc}), args.cpu_seconds / 3, seed=seed)
+    return {"value": res[1], "unit": "GB/s", "cores": 1, "kind": "port", "value_all_cores": res[allc],
+            "cores_all": allc, "verified": bool(ok),
+            "sample": f"1 whole stripe of CL(k={k},r={r},m={m}) B={mib} MiB: encodeData flow + decodeData of D0"}
+
+
 def main():
     argv = sys.argv[1:]
     args = parse(argv)
@@ -1097,13 +1198,23 @@ def main():
     if args.shape_steps > 0 and not pl["hbm_fill"] and not args.strong:
         for leg_def in SHAPE_LEGS:
             line[leg_def[0]] = shape_leg(args, d, E, leg_def)
-    d.barrier()  # the rank-0-only host legs below never overlap another rank's timed region
+    d.barrier()  # the host legs below never overlap another rank's device-resident timed region
+    if args.host_iters > 0:
+        # every rank at once: the node's PCIe links and host DRAM together
+        line["host_resident"] = host_resident_leg(args, d, args.host_iters)
+    d.barrier()
     if d.rank == 0:
-        if args.cpu_seconds > 0:
+        # CPU baselines: rank 0 at N = 1 only (a bounded sample of each workload on this host's cores)
+        cpu_on = args.cpu_seconds > 0 and d.world == 1
+        if cpu_on:
             line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)
+            for leg_def in SHAPE_LEGS:
+                if leg_def[0] in line:
+                    line[leg_def[0]]["cpu_baseline"] = shape_cpu_baseline(args, leg_def)
+        elif args.cpu_seconds > 0:
+            line["cpu_baseline_note"] = "measured at N = 1 only (BENCH); the same host CPU path at every N"
         if args.host_iters > 0:
-            line["host_resident"] = host_resident_leg(args, d.dev, args.host_iters)
-            line["host_resident"]["chunk_generator"] = chunkgen_leg(args)
+            line["host_resident"]["chunk_generator"] = chunkgen_leg(args, args.cpu_seconds / 4 if cpu_on else 0.0)
         print(json.dumps(line), flush=True)
     d.close()
 

@@ -97,6 +97,9 @@ SIGNATURES = {
     "ecw_repair_sources": (c_int, [c_void_p, c_int, POINTER(c_int), c_int]),
     "ecw_service_counters": (c_int, [c_int, POINTER(c_uint64)]),
     "ecw_set_schedule": (c_int, [POINTER(ecw_schedule)]),
+    "ecw_host_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p), POINTER(c_int)]),
+    "ecw_host_free": (c_int, [c_void_p]),
+    "ecw_device_numa_node": (c_int, [c_int]),
     "ecw_get_schedule": (c_int, [POINTER(ecw_schedule)]),
     "ecw_fill_random_dev": (c_int, [c_int, c_void_p, c_size_t, c_size_t, c_int, c_int, c_size_t, c_uint64, c_int,
                                     c_int, c_void_p]),

@@ -37,6 +37,20 @@ def up_to_date(out=OUT, sources=SOURCES) -> bool:
     return all(os.path.getmtime(p) <= t for p in sources + HEADERS + [__file__])
 
 
+def includes(src: str, seen=None) -> set:
+    """`src` and every file it includes with #include "..." (recursively)."""
+    import re
+
+    seen = set() if seen is None else seen
+    src = os.path.normpath(src)
+    if src in seen or not os.path.exists(src):
+        return seen
+    seen.add(src)
+    for name in re.findall(r'^#include "([^"]+)"', open(src).read(), flags=re.M):
+        includes(os.path.join(os.path.dirname(src), name), seen)
+    return seen
+
+
 def compile_lib(out: str, extra=(), obj_dir: str = OBJ) -> None:
     """Every translation unit to an object in parallel (the kernel TUs take
     minutes each: encode, XOR and service are separate so they compile side
@@ -46,8 +60,15 @@ def compile_lib(out: str, extra=(), obj_dir: str = OBJ) -> None:
 
     os.makedirs(obj_dir, exist_ok=True)
 
+    stamp = os.path.join(obj_dir, "flags.txt")  # objects built with other flags are rebuilt
+    flags = " ".join([*FLAGS_C, *extra])
+    same_flags = os.path.exists(stamp) and open(stamp).read() == flags
+
     def one(src):
         o = os.path.join(obj_dir, os.path.basename(src) + ".o")
+        if same_flags and os.path.exists(o) and os.path.getmtime(o) >= max(
+                os.path.getmtime(p) for p in [__file__, *includes(src)]):
+            return o
         cmd = [HIPCC, *FLAGS_C, *extra, "-c", src, "-o", o + _tmp()]
         subprocess.run(cmd, check=True)
         os.replace(o + _tmp(), o)
@@ -55,6 +76,8 @@ def compile_lib(out: str, extra=(), obj_dir: str = OBJ) -> None:
 
     with ThreadPoolExecutor(max_workers=len(SOURCES)) as ex:
         objs = list(ex.map(one, SOURCES))
+    with open(stamp, "w") as f:
+        f.write(flags)
     subprocess.run([HIPCC, "--offload-arch=gfx950", "-shared", "-fPIC", *objs, "-o", out + _tmp()], check=True)
     os.replace(out + _tmp(), out)
 

@@ -387,6 +387,13 @@ def set_schedule(**fields) -> dict:
     return prev
 
 
+def apply_schedule(L, **fields) -> None:
+    """ecw_set_schedule on a given build `L` (a tuning variant loaded with
+    _lib.load(path, strict=False)); fields not given go back to -1."""
+    s = _lib.ecw_schedule(*[int(fields.get(f, -1)) for f in SCHEDULE_FIELDS])
+    _check(L.ecw_set_schedule(byref(s)), f"set_schedule({fields})")
+
+
 def parse_schedule(xor: str | None = None, window: str | None = None, remap: str | None = None) -> dict:
     """Schedule fields from the string forms the tools and the environment use:
     xor = "K,ORDER[,LOG2P,W]" (a whole XOR schedule: no window unless given),
@@ -409,3 +416,26 @@ def parse_schedule(xor: str | None = None, window: str | None = None, remap: str
     if remap not in (None, "auto"):
         f["xcd_remap"] = int(remap)
     return f
+
+
+class PinnedHost:
+    """Host memory on the NUMA node of `device`'s PCIe root, pinned for DMA
+    (ecw_host_alloc): staging for the host-memory entry points that keeps
+    their copies at PCIe rate and off the inter-socket fabric. `.array` is a
+    uint8 numpy view; `.numa_node` the node its pages were found on (-1:
+    unknown). Freed by free() or when the object is collected."""
+
+    def __init__(self, nbytes: int, device: int = 0):
+        import weakref
+
+        p, node = c_void_p(), c_int(-1)
+        _check(lib.ecw_host_alloc(device, nbytes, byref(p), byref(node)), f"host_alloc({nbytes})")
+        self.ptr, self.nbytes, self.device = p.value, int(nbytes), device
+        self.numa_node = node.value
+        self.device_numa_node = lib.ecw_device_numa_node(device)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+        self._fin = weakref.finalize(self, lib.ecw_host_free, c_void_p(self.ptr))
+
+    def free(self) -> None:
+        self.array = None
+        self._fin()

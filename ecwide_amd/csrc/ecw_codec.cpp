@@ -24,6 +24,10 @@
 #include <thread>
 #include <vector>
 
+#include <sys/mman.h>
+#include <sys/syscall.h>
+#include <unistd.h>
+
 #include "../../include/ecwide.h"
 #include "ecw_gf.hpp"
 #include "ecw_internal.hpp"
@@ -562,6 +566,36 @@ Schedule& schedule_locked() {
   }
   return g_sched;
 }
+
+// ---- NUMA-local pinned host staging (ecw_host_alloc) ------------------------
+// The GPU's NUMA node from sysfs (-1: unknown, e.g. a host without NUMA).
+int device_numa_node(int device) {
+  char bdf[64] = {};
+  if (hipDeviceGetPCIBusId(bdf, sizeof bdf, device) != hipSuccess) return -1;
+  for (char* p = bdf; *p; ++p) *p = static_cast<char>(std::tolower(static_cast<unsigned char>(*p)));
+  std::ifstream f(std::string("/sys/bus/pci/devices/") + bdf + "/numa_node");
+  int node = -1;
+  if (!(f >> node)) return -1;
+  return node;
+}
+
+// Node of the pages of [p, p + n) by sampling up to 64 of them (move_pages
+// with no target nodes only reports): the node they all sit on, -1 if they
+// are spread or the kernel does not tell.
+int pages_node(void* p, size_t n) {
+  const size_t pg = 4096, npages = (n + pg - 1) / pg, samples = std::min<size_t>(64, npages);
+  std::vector<void*> pages(samples);
+  std::vector<int> status(samples, -1);
+  for (size_t i = 0; i < samples; ++i)
+    pages[i] = static_cast<char*>(p) + (npages * i / samples) * pg;
+  if (syscall(SYS_move_pages, 0, samples, pages.data(), nullptr, status.data(), 0) != 0) return -1;
+  for (size_t i = 1; i < samples; ++i)
+    if (status[i] != status[0]) return -1;
+  return status[0] >= 0 ? status[0] : -1;
+}
+
+std::mutex g_host_mu;
+std::map<void*, size_t> g_host_allocs;  // ecw_host_alloc'd regions (mapped bytes)
 
 }  // namespace
 
@@ -1607,6 +1641,69 @@ extern "C++" int counters(int device, unsigned long long out[4]) {
 }
 
 }  // namespace svc
+
+int ecw_host_alloc(int device, size_t bytes, void** out, int* numa_node) {
+  if (!out || bytes == 0 || device < 0) return ECW_EINVAL;
+  *out = nullptr;
+  if (numa_node) *numa_node = -1;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return ECW_EDEVICE;
+  const int node = device_numa_node(device);
+  const size_t n = (bytes + 4095) & ~static_cast<size_t>(4095);
+  void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+  if (p == MAP_FAILED) return ECW_ENOMEM;
+  if (node >= 0 && node < 1024) {
+    // preferred (not bound): a full node falls back to another instead of failing
+    unsigned long mask[16] = {};
+    mask[node / 64] = 1ul << (node % 64);
+    (void)syscall(SYS_mbind, p, n, 1 /* MPOL_PREFERRED */, mask, 1024ul, 0u);
+  }
+  // fault every page in (on the preferred node) from several threads
+  const unsigned nt = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  const size_t per = (n / nt + 4095) & ~static_cast<size_t>(4095);
+  std::vector<std::thread> th;
+  for (unsigned t = 0; t < nt; ++t) {
+    const size_t o = t * per;
+    if (o >= n) break;
+    th.emplace_back([=] { std::memset(static_cast<char*>(p) + o, 0, std::min(per, n - o)); });
+  }
+  for (auto& x : th) x.join();
+  {
+    DeviceGuard g(device);
+    if (!g.ok || hipHostRegister(p, n, hipHostRegisterDefault) != hipSuccess) {
+      munmap(p, n);
+      return ECW_EDEVICE;
+    }
+  }
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    g_host_allocs[p] = n;
+  }
+  if (numa_node) *numa_node = pages_node(p, n);
+  *out = p;
+  return ECW_OK;
+}
+
+int ecw_host_free(void* p) {
+  if (!p) return ECW_OK;
+  size_t n = 0;
+  {
+    std::lock_guard<std::mutex> lk(g_host_mu);
+    auto it = g_host_allocs.find(p);
+    if (it == g_host_allocs.end()) return ECW_EINVAL;
+    n = it->second;
+    g_host_allocs.erase(it);
+  }
+  const int st = hipHostUnregister(p) == hipSuccess ? ECW_OK : ECW_EDEVICE;
+  munmap(p, n);
+  return st;
+}
+
+int ecw_device_numa_node(int device) {
+  int ndev = 0;
+  if (device < 0 || hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return -1;
+  return device_numa_node(device);
+}
 
 int ecw_service_counters(int device, unsigned long long out[4]) {
   if (!out || device < 0) return ECW_EINVAL;

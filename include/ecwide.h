@@ -193,6 +193,22 @@ int ecw_encode_stripes(ecw_codec* codec, int stripes, const uint8_t* const* data
  * `out` receives the rebuilt `lost_block` (D or L). */
 int ecw_repair(ecw_codec* codec, const uint8_t* const* blocks, int lost_block, uint8_t* out, size_t len);
 
+/* NUMA-local pinned host staging for the host-memory entry points. The
+ * reference's blocks are host buffers (Java direct ByteBuffers filled from
+ * files, BufferUnit.java:53-68, FileOp.java:7-21); the host-memory calls move
+ * them over PCIe, at DMA rate only from pinned memory, and across the
+ * inter-socket fabric when the buffer sits on the other socket's DRAM.
+ * ecw_host_alloc maps `bytes` (rounded up to 4 KiB) of zeroed host memory
+ * with its pages preferred on the NUMA node of `device`'s PCIe root (sysfs),
+ * faults them in and registers them with the GPU runtime (pinned).
+ * *numa_node (optional) receives the node the pages were found on (sampled;
+ * -1 when unknown or spread). Free with ecw_host_free. No reference
+ * counterpart (placement of the caller's buffers). ECW_EDEVICE without a GPU. */
+int ecw_host_alloc(int device, size_t bytes, void** out, int* numa_node);
+int ecw_host_free(void* ptr);
+/* NUMA node of `device` (-1 when unknown or no such device). */
+int ecw_device_numa_node(int device);
+
 /* Counters of the resident small-request service on `device` (host-memory
  * calls of blocks up to 64 KiB: ecw_encode of one stripe, and the XORs of
  * ecw_decode / ecw_partial_decode / ecw_repair / ecw_xor_intermediate), for

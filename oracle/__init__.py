@@ -61,6 +61,7 @@ class Oracle:
         L.orc_init_tables.argtypes = [c_int, c_int, _u8p, _u8p]
         for f in (L.orc_encode_data_base, L.orc_encode_data_avx2):
             f.argtypes = [c_int, c_int, c_int, _u8p, _u8pp, _u8pp]
+        L.orc_encode_data_avx2_mt.argtypes = [c_int, c_int, c_int, _u8p, _u8pp, _u8pp, c_int]
         L.orc_codec_new.restype = c_void_p
         L.orc_codec_new.argtypes = [c_char, c_int, c_int, c_int, c_int, c_int, c_int]
         L.orc_codec_free.argtypes = [c_void_p]

@@ -411,6 +411,47 @@ void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int 
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
 
+/* ec_encode_data (AVX2 port) split by byte range over nthreads threads: the
+ * multi-threaded form of decodeData / a CL repair (NativeCodec.cc:237-248:
+ * ec_encode_data with the all-ones table) for the CPU baseline. */
+typedef struct {
+  int len, k, rows;
+  const uint8_t* tbl;
+  uint8_t* src[256];
+  uint8_t* dst[256];
+} ed_job;
+
+static void* ed_run(void* arg) {
+  ed_job* j = (ed_job*)arg;
+  orc_encode_data_avx2(j->len, j->k, j->rows, j->tbl, j->src, j->dst);
+  return NULL;
+}
+
+void orc_encode_data_avx2_mt(int len, int k, int rows, const uint8_t* tbl, uint8_t** src, uint8_t** dst,
+                             int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (nthreads > 256) nthreads = 256;
+  int per = (len / nthreads) & ~63;
+  if (nthreads == 1 || per < 64 || k > 256 || rows > 256) {
+    orc_encode_data_avx2(len, k, rows, tbl, src, dst);
+    return;
+  }
+  pthread_t th[256];
+  ed_job* jobs = (ed_job*)malloc(sizeof(ed_job) * nthreads);
+  for (int t = 0; t < nthreads; ++t) {
+    const int off = t * per;
+    jobs[t].len = (t == nthreads - 1) ? len - off : per;
+    jobs[t].k = k;
+    jobs[t].rows = rows;
+    jobs[t].tbl = tbl;
+    for (int i = 0; i < k; ++i) jobs[t].src[i] = src[i] + off;
+    for (int i = 0; i < rows; ++i) jobs[t].dst[i] = dst[i] + off;
+    pthread_create(&th[t], NULL, ed_run, &jobs[t]);
+  }
+  for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
+  free(jobs);
+}
+
 /* ---------------- synthetic data (ecwide.h, ecw_fill_random_dev) ---------------- */
 static uint64_t mix64(uint64_t z) {
   z ^= z >> 30;

@@ -910,6 +910,33 @@ def test_host_pipeline_multi_chunk_and_repair(E, torch, orc, B):
         assert np.array_equal(out, blocks[lost]), lost
 
 
+def test_pinned_host_numa_local_pipeline(E, orc):
+    """ecw_host_alloc (PinnedHost): zeroed, pinned host memory on the GPU's NUMA
+    node (when the host reports one); the host pipeline encodes and repairs
+    through it bit-exact vs the oracle; freeing twice is refused, not a crash."""
+    k, m, r, B = 20, 3, 5, (9 << 20) + 48  # two 8 MiB pipeline slices + a ragged tail
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    np_ = c.parityNum
+    h = E.PinnedHost((k + np_ + 1) * B, c.device)
+    assert h.array.size == (k + np_ + 1) * B and not h.array[:: 1 << 20].any()
+    if h.device_numa_node >= 0:
+        assert h.numa_node == h.device_numa_node, (h.numa_node, h.device_numa_node)
+    v = [h.array[i * B:(i + 1) * B] for i in range(k + np_ + 1)]
+    data = [orc.fill(B, 31, 0, j) for j in range(k)]
+    for j in range(k):
+        v[j][:] = data[j]
+    c.encodeData(v[:k], v[k:k + np_])
+    want = orc.codec("C", k, m, r, B).encode(data, threads=8)
+    assert all(np.array_equal(a, b) for a, b in zip(v[k:k + np_], want))
+    c.repairBlock(v[:k + np_], 0, v[k + np_])
+    assert np.array_equal(v[k + np_], data[0])
+    ptr = h.ptr
+    h.free()
+    from ctypes import c_void_p
+
+    assert E._lib.lib.ecw_host_free(c_void_p(ptr)) == -1  # already freed: refused
+
+
 @pytest.mark.parametrize("k,m,r,B", [(32, 3, 11, 65536 + 16), (128, 3, 27, 1 << 16), (20, 2, 5, 4096)])
 def test_multinode_encode_chain(E, torch, orc, k, m, r, B):
     """Multi-node CL encode (ECTaskProcessor.java:267-291): each of the g

@@ -259,3 +259,19 @@ def test_schedule_seeded_from_environment_once():
                          cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
     assert eval(out.stdout.strip()) == {f: -1 for f in E.codec.SCHEDULE_FIELDS}
     assert "ECW_XOR_SCHED" in out.stderr and "ECW_WRITE_WINDOW" in out.stderr
+
+
+def test_host_alloc_without_gpu_fails_cleanly():
+    """ecw_host_alloc / ecw_host_free / ecw_device_numa_node on a host without
+    a GPU: status codes, no crash, nothing leaked or mapped."""
+    from ctypes import byref, c_int, c_void_p
+
+    p, node = c_void_p(), c_int(7)
+    assert _lib.lib.ecw_host_alloc(0, 1 << 20, byref(p), byref(node)) == -3  # ECW_EDEVICE
+    assert p.value is None and node.value == -1
+    assert _lib.lib.ecw_host_alloc(0, 0, byref(p), None) == -1  # ECW_EINVAL
+    assert _lib.lib.ecw_host_free(None) == 0
+    assert _lib.lib.ecw_host_free(c_void_p(4096)) == -1  # not ours
+    assert _lib.lib.ecw_device_numa_node(0) == -1
+    with pytest.raises(E.EcwError):
+        E.PinnedHost(4096)

@@ -215,6 +215,10 @@ def test_bench_dry_run_n8_per_rank_fields():
     assert line["configs1"]["block_bytes"] == 16 << 20
     assert line["configs0_shape"]["stripes_per_gpu"] == 8 and line["configs0_shape"]["block_bytes"] == 64 << 20
     assert len(line["configs0_shape"]["rank_ms_per_step"]) == 8
+    # the host-resident leg runs on every rank, its own pinned stripe each
+    h = line["host_resident"]
+    for key in ("rank_GBps", "rank_h2d_GBps", "rank_numa_node", "rank_gpu_numa_node"):
+        assert len(h[key]) == 8, key
 
 
 def test_bench_dry_run_strong_and_column_modes():

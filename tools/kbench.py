@@ -4,8 +4,8 @@ same data, rounds interleaved: cdna_hip_programming.md §5.4 rule 24).
 
   python tools/kbench.py [--k 128 --m 3 --r 27 --mib 64 --stripes 4 --rounds 5] build/variants/*.so
 
-A lib given as PATH@VALUE runs with ECW_WRITE_WINDOW=VALUE set around its calls
-(the encode's write-window choice is read per launch), so one build can be
+A lib given as PATH@VALUE runs with the encode write window VALUE (off | on |
+LOG2P,W; ecw_set_schedule) set around its calls, so one build can be
 A/B-ed against itself: ecwide_amd/libecwide.so@off ecwide_amd/libecwide.so@on.
 """
 import argparse
@@ -50,6 +50,7 @@ def main():
     import torch
 
     from ecwide_amd import _lib
+    from ecwide_amd.codec import apply_schedule, parse_schedule
 
     k, m, r = a.k, a.m, a.r
     B = int(a.mib * (1 << 20))
@@ -116,10 +117,8 @@ def main():
     res = {n: ([], []) for n, _, _ in libs}
     for rd in range(a.rounds):
         for name, L, h in libs:
-            if envs[name]:
-                os.environ["ECW_WRITE_WINDOW"] = envs[name]
-            else:
-                os.environ.pop("ECW_WRITE_WINDOW", None)
+            if hasattr(L, "ecw_set_schedule"):  # (builds before round 5 read ECW_WRITE_WINDOW per launch)
+                apply_schedule(L, **parse_schedule(window=envs[name] or None))
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             for it in range(a.iters + 1):
                 if it == 1:

@@ -11,12 +11,12 @@ Placements (S stripes of CL(k, r, m), B-byte blocks):
   sep       every block its own torch.empty(B) (the bench's pointer leg)
   carved0   pointer tables into one allocation, block stride exactly B
   carved4k  the same at block stride B + 4 KiB
-Schedules (ECW_XOR_SCHED = "K,ORDER[,LOG2P,W]", ecw_kernels.hip launch_xor_range):
+Schedules ("K,ORDER[,LOG2P,W]", set with ecw_set_schedule; ecw_xor.hpp launch_xor_range):
   K tiles per workgroup read diagonally, ORDER 1 = column-major groups,
   LOG2P,W = write window; "auto" = the library's choice; a "+r" suffix (also on
-  --enc-windows settings) adds the per-XCD tile order (ECW_XCD_REMAP=1).
+  --enc-windows settings) adds the per-XCD tile order (xcd_remap = 1).
 
-  python tools/repair_ab.py --lib build/variants/skewall.so [--stripes 4] [--scheds 1,0 4,0 ...]
+  python tools/repair_ab.py [--lib build/variants/X.so] [--stripes 4] [--scheds 1,0 2,0 4,0 ...]
 """
 import argparse
 import ctypes
@@ -39,16 +39,18 @@ def main():
     ap.add_argument("--stripes", type=int, default=4)
     ap.add_argument("--chunk", type=int, default=8192, help="column piece of the tiled placement")
     ap.add_argument("--placements", default="tiled,split,sep,carved0,carved4k")
-    ap.add_argument("--scheds", nargs="+", default=["1,0", "4,0", "1,1", "4,1", "1,0,11,64", "2,0", "8,0"])
+    ap.add_argument("--scheds", nargs="+", default=["1,0", "2,0", "4,0", "1,1", "4,1", "1,0,11,64", "4,0,11,64"])
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--encode", action="store_true", help="also time the encode of every placement")
     ap.add_argument("--enc-windows", nargs="*", default=[],
-                    help="with --encode: ECW_WRITE_WINDOW settings to time the encode under (auto = unset)")
+                    help="with --encode: encode write-window settings to time the encode under "
+                         "(off | on | LOG2P,W; auto = the library's choice)")
     a = ap.parse_args()
     import torch
 
     from ecwide_amd import _lib
+    from ecwide_amd.codec import apply_schedule, parse_schedule
 
     L = _lib.load(a.lib, strict=False)
     k, m, r, S = a.k, a.m, a.r, a.stripes
@@ -154,15 +156,8 @@ def main():
         order = combos[rd % len(combos):] + combos[:rd % len(combos)]
         for p, sc in order:
             enc, rep, d0 = legs[p]
-            base, _, rflag = sc.partition("+")  # "+r": the per-XCD tile order (ECW_XCD_REMAP=1)
-            if rflag == "r":
-                os.environ["ECW_XCD_REMAP"] = "1"
-            else:
-                os.environ.pop("ECW_XCD_REMAP", None)
-            if base == "auto":
-                os.environ.pop("ECW_XOR_SCHED", None)  # the library's own choice
-            else:
-                os.environ["ECW_XOR_SCHED"] = base
+            base, _, rflag = sc.partition("+")  # "+r": the per-XCD tile order
+            apply_schedule(L, **parse_schedule(xor=base, remap="1" if rflag == "r" else None))
             assert rep() == 0
             e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
             e[0].record()
@@ -180,14 +175,7 @@ def main():
                 rr[1].append(enc_bytes * a.iters / (e[1].elapsed_time(e[2]) * 1e-3) / 1e9)
                 for wv in a.enc_windows:  # the encode under other write-window settings, same round
                     wbase, _, rflag = wv.partition("+")
-                    if rflag == "r":
-                        os.environ["ECW_XCD_REMAP"] = "1"
-                    else:
-                        os.environ.pop("ECW_XCD_REMAP", None)
-                    if wbase == "auto":
-                        os.environ.pop("ECW_WRITE_WINDOW", None)
-                    else:
-                        os.environ["ECW_WRITE_WINDOW"] = wbase
+                    apply_schedule(L, **parse_schedule(window=wbase, remap="1" if rflag == "r" else None))
                     f = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
                     enc()
                     f[0].record()
@@ -196,13 +184,12 @@ def main():
                     f[1].record()
                     torch.cuda.synchronize()
                     encw.setdefault((p, wv), []).append(enc_bytes * a.iters / (f[0].elapsed_time(f[1]) * 1e-3) / 1e9)
-                os.environ.pop("ECW_WRITE_WINDOW", None)
-                os.environ.pop("ECW_XCD_REMAP", None)
+                apply_schedule(L)
             if rd == 0:
                 ok = all(torch.equal(out[s * B:(s + 1) * B], d0[s]()) for s in range(S))
                 if not ok:
                     print(f"  !! {p} sched {sc}: repair != D0", flush=True)
-    os.environ.pop("ECW_XOR_SCHED", None)
+    apply_schedule(L)
     print(f"CL(k={k},r={r},m={m}) B={a.mib} MiB x{S} stripes, repair of D0 ({nsrc} sources): GB/s median "
           f"(min..max) over {a.rounds} interleaved rounds; lib {os.path.basename(a.lib)}")
     for (p, sc), (rp, en) in res.items():

@@ -53,10 +53,7 @@ def run(a):
     d0 = {"sep": lambda: data[0][0], "split": lambda: split.block(0, 0)}
     ok = True
     for place, sched in LEGS:
-        if sched == "auto":
-            os.environ.pop("ECW_XOR_SCHED", None)
-        else:
-            os.environ["ECW_XOR_SCHED"] = sched
+        E.set_schedule(**E.parse_schedule(xor=sched))
         e = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
         e[0].record()
         for _ in range(a.reps):
@@ -68,7 +65,7 @@ def run(a):
               f"{S * (r + 1) * B / (ms * 1e-3) / 1e9:.1f} GB/s", flush=True)
         ok = ok and torch.equal(out[:B], d0[place]())  # (both placements repair into `out`)
     print(f"repairs == D0: {ok}")
-    os.environ.pop("ECW_XOR_SCHED", None)
+    E.set_schedule()
     tiled = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled")
     tiled.fill_random(seed=5)
     assert tiled.encode_launches() == ENC_LAUNCHES and split.encode_launches() == ENC_LAUNCHES
