@@ -9,6 +9,7 @@
 // and the sanitizers stayed quiet.
 #include <jni.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -279,10 +280,44 @@ static void fastdiv() {
           (static_cast<uint64_t>(ecw::stripes_per_launch(t)) + 1) * t >= (1ull << 31));
 }
 
+// ecw_set_schedule / ecw_get_schedule from 8 threads at once (the launchers
+// take one copy per launch under the same lock), out-of-range values refused;
+// ecw_host_alloc / ecw_host_free without a GPU: status codes, nothing leaked.
+static void schedule_and_host() {
+  std::vector<std::thread> th;
+  std::atomic<int> bad{0};
+  for (int t = 0; t < 8; ++t)
+    th.emplace_back([t, &bad] {
+      for (int i = 0; i < 200; ++i) {
+        ecw_schedule s = {1 << (i % 3), t & 1, 10 + (i % 3), 32 * (i % 2), -1, i % 2 ? 0 : -1, (t + i) & 1};
+        if (ecw_set_schedule(&s) != ECW_OK) ++bad;
+        ecw_schedule g;
+        if (ecw_get_schedule(&g) != ECW_OK || (g.xor_skew != 1 && g.xor_skew != 2 && g.xor_skew != 4)) ++bad;
+      }
+    });
+  for (auto& x : th) x.join();
+  CHECK(bad == 0);
+  ecw_schedule s = {3, -1, -1, -1, -1, -1, -1};
+  CHECK(ecw_set_schedule(&s) == ECW_EINVAL);
+  s = ecw_schedule{-1, -1, 30, -1, -1, -1, -1};
+  CHECK(ecw_set_schedule(&s) == ECW_EINVAL);
+  CHECK(ecw_set_schedule(nullptr) == ECW_OK);
+  CHECK(ecw_get_schedule(&s) == ECW_OK && s.xor_skew == -1 && s.enc_window_width == -1);
+  CHECK(ecw_get_schedule(nullptr) == ECW_EINVAL);
+  void* p = reinterpret_cast<void*>(1);
+  int node = 5;
+  CHECK(ecw_host_alloc(0, 1 << 20, &p, &node) == ECW_EDEVICE && p == nullptr && node == -1);
+  CHECK(ecw_host_alloc(0, 0, &p, nullptr) == ECW_EINVAL);
+  CHECK(ecw_host_free(nullptr) == ECW_OK);
+  CHECK(ecw_host_free(&node) == ECW_EINVAL);
+  CHECK(ecw_device_numa_node(0) == -1);
+}
+
 int main() {
   fastdiv();
   schemes();
   codecs();
+  schedule_and_host();
   isal_shim();
   jni();
   std::printf("asan_host: %d checks, %d failed\n", g_checks, g_fail);
