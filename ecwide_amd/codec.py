@@ -433,9 +433,12 @@ class PinnedHost:
         self.ptr, self.nbytes, self.device = p.value, int(nbytes), device
         self.numa_node = node.value
         self.device_numa_node = lib.ecw_device_numa_node(device)
-        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * self.nbytes).from_address(self.ptr))
+        raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
+        raw.owner = self  # views of `array` keep the allocation alive (freed when the last one goes)
+        self.array = np.ctypeslib.as_array(raw)
         self._fin = weakref.finalize(self, lib.ecw_host_free, c_void_p(self.ptr))
 
     def free(self) -> None:
+        """Unregister and unmap now: views of `array` must not be used after."""
         self.array = None
         self._fin()

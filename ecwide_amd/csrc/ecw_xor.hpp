@@ -247,22 +247,32 @@ struct XorChoice {
 //    n = 9 6550-6558 against 6191-6320 without it. Below 8 sources a tile's
 //    reads take too few window periods and the window locks the workgroups
 //    into generations (n = 4: -2..-10 %; K = 1 with the window: -50..-70 %);
-//  * the tiled slab's 8 KiB units keep K = 1 and no window (K = 4: -0.5..-8 %,
-//    window -2..-70 %: its sources are one contiguous run already).
-// Column-major group order and K = 2 / 8 gained less than K = 4 everywhere.
-//  * round 4, later: the tiled slab's 16 KiB units (k <= 32, slab.default_chunk)
-//    are one whole group of K = 4 tiles and take the same schedule: CL(32, 8, 2)
-//    6240 -> 6379, CL(32, 11, 3) 6259 -> 6537 GB/s (profiles/r04_k32r_cfg1/0.log);
-//    K = 2 on the 8 KiB units of k = 128: +0.5 % with the window, -2 % without
-//    (r04_k128r_tiled.log), so they keep K = 1.
+//  * column-major group order and K = 8 gained less than K = 4 for whole blocks;
+//  * the tiled slab's 16 KiB units (k <= 32, slab.default_chunk) are one whole
+//    group of K = 4 tiles and take the same schedule: CL(32, 8, 2) 6240 -> 6379,
+//    CL(32, 11, 3) 6259 -> 6537 GB/s (profiles/r04_k32r_cfg1/0.log);
+//  * round 5: the tiled slab's 8 KiB units (k = 128, the bench's headline) are
+//    one whole group of K = 2 tiles and take K = 2 + the window, chosen by the
+//    WORST of five tiled slabs allocated side by side in one process (where an
+//    allocation lands sets +-3-6 %; tools/repair_placement.py, two processes,
+//    profiles/r05_placement_1/2.log): worst slab 6145 / 6189 GB/s with round 4's
+//    K = 1 and no window, 6467 / 6466 with K = 2 + window (median 6552 / 6592,
+//    best 6594 / 6611 against 6637 / 6628), 0.983 / 0.987 of the split slab's
+//    own default in the same process. K = 4 + window was the worst (6090 / 6167:
+//    a 2-tile unit is a ragged group of 4, reduced tile by tile), K = 2 without
+//    the window no better than K = 1, a 2^10 / 32 window between (6320 / 6340);
 //  * the XOR keeps the dispatch tile order (the per-XCD order: -0.4..-5 %,
 //    profiles/r04_remap_*.log).
 inline XorChoice xor_choice(const XorGeom& g) {
   constexpr uint64_t group = static_cast<uint64_t>(kXorSkewWhole) * kTileBytes;
+  const uint64_t tiles = static_cast<uint64_t>(g.stripes) * g.tiles;
   const bool whole = g.len >= 65536 || (g.len >= group && g.len % group == 0);
+  // units of exactly two tiles (the tiled slab's 8 KiB pieces), wide enough
+  // for the window
+  const bool pair = !whole && g.len == 2 * kTileBytes && g.n >= 8 && tiles >= 8192;
   const Schedule sc = current_schedule();
-  XorChoice c{whole ? kXorSkewWhole : 1, 0, 11, 0, 0};
-  if (whole && g.n >= 8 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192) c.wwidth = 64;
+  XorChoice c{whole ? kXorSkewWhole : pair ? 2 : 1, 0, 11, 0, 0};
+  if ((whole || pair) && g.n >= 8 && tiles >= 8192) c.wwidth = 64;
   if (sc.xor_skew > 0) c.skew = sc.xor_skew;
   if (sc.xor_order >= 0) c.order = static_cast<uint32_t>(sc.xor_order);
   if (sc.xor_width >= 0) {

@@ -133,38 +133,65 @@ def run(a):
         print("split slab: " + " ".join(f"{sc}={x:.1f}" for sc, x in zip(a.scheds, sv)))
 
 
+def _csv_rows(path):
+    with open(path) as f:
+        yield from csv.DictReader(f)
+
+
 def summarize(a):
+    """Counters (and, with a kernel trace of the same run, durations) per
+    (slab, schedule); per schedule the slowest and fastest tiled slab side by
+    side -- what the worst placement pays for."""
     per = defaultdict(lambda: defaultdict(float))
-    eper = defaultdict(lambda: defaultdict(float))
+    dur = {}
     for path in a.summarize:
-        with open(path) as f:
-            for row in csv.DictReader(f):
-                name = row.get("Kernel_Name", "")
-                tgt = per if "xor_kernel_fixed" in name else eper if "encode_kernel_asm" in name else None
-                if tgt is None:
-                    continue
-                tgt[int(row["Dispatch_Id"])][row["Counter_Name"]] += float(row["Counter_Value"])
-    ids = sorted(per)
+        for row in _csv_rows(path):
+            name = row.get("Kernel_Name", "")
+            if "xor_kernel_fixed" not in name:
+                continue
+            d = int(row["Dispatch_Id"])
+            if "Counter_Name" in row:
+                per[d][row["Counter_Name"]] += float(row["Counter_Value"])
+            elif "Start_Timestamp" in row:
+                dur[d] = (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-6  # ms
+    ids = sorted(per or dur)
     L = legs(a)
-    # the correctness pass dispatches every leg once first
-    ids = ids[len(L):]
+    ids = ids[len(L):]  # the correctness pass dispatches every leg once first
     if len(ids) != len(L) * a.pmc_reps:
         print(f"warning: {len(ids)} timed xor dispatches, expected {len(L) * a.pmc_reps}")
     B, S = a.mib << 20, a.stripes
+    alg = S * (a.r + 1) * B
+    res = {}
     for i, (n, sc) in enumerate(L):
         grp = ids[i * a.pmc_reps:(i + 1) * a.pmc_reps]
         if not grp:
             break
         cs = sorted({c for d in grp for c in per[d]})
         avg = {c: sum(per[d][c] for d in grp) / len(grp) for c in cs}
-        extra = ""
+        ms = sum(dur[d] for d in grp if d in dur) / max(1, sum(1 for d in grp if d in dur)) if dur else None
+        res[(n, sc)] = (avg, ms)
+    def line(n, sc):
+        avg, ms = res[(n, sc)]
+        extra = f" {ms:.4f} ms = {alg / (ms * 1e-3) / 1e9:.1f} GB/s" if ms else ""
         if avg.get("TCC_EA0_RDREQ_sum") and "TCC_EA0_RDREQ_LEVEL_sum" in avg:
-            extra += f" read level/req {avg['TCC_EA0_RDREQ_LEVEL_sum'] / avg['TCC_EA0_RDREQ_sum']:.1f}"
+            extra += f" | read level/req {avg['TCC_EA0_RDREQ_LEVEL_sum'] / avg['TCC_EA0_RDREQ_sum']:.1f}"
+        if avg.get("TCC_EA0_WRREQ_sum") and "TCC_EA0_WRREQ_LEVEL_sum" in avg:
+            extra += f" | write level/req {avg['TCC_EA0_WRREQ_LEVEL_sum'] / avg['TCC_EA0_WRREQ_sum']:.1f}"
         if "FETCH_SIZE" in avg:
-            extra += f" read/alg {avg['FETCH_SIZE'] * 1024 * 2 / (S * a.r * B):.5f}"
-        print(f"{n:3s} {sc:11s} " + " ".join(f"{c}={v:.4g}" for c, v in avg.items()) + extra)
-    eids = sorted(eper)
-    print(f"encode dispatches: {len(eids)} (the last {a.pmc_reps * 2} per slab, slab order)")
+            extra += f" | read/alg {avg['FETCH_SIZE'] * 1024 * 2 / (S * a.r * B):.5f}"
+        if "WRITE_SIZE" in avg:
+            extra += f" | write/alg {avg['WRITE_SIZE'] * 1024 / (S * B):.5f}"
+        return f"{n:3s} {sc:11s}{extra} | " + " ".join(f"{c}={v:.4g}" for c, v in avg.items())
+    for n, sc in L:
+        if (n, sc) in res:
+            print(line(n, sc))
+    if dur:
+        print("per schedule: slowest / fastest tiled slab (this run's own durations)")
+        for sc in a.scheds:
+            tl = [(res[(n, sc)][1], n) for n, s2 in L if s2 == sc and n.startswith("T") and (n, sc) in res]
+            if tl:
+                print("  slowest " + line(max(tl)[1], sc))
+                print("  fastest " + line(min(tl)[1], sc))
 
 
 if __name__ == "__main__":
