@@ -100,7 +100,9 @@ def run(a):
         return
     rep = defaultdict(list)
     enc = defaultdict(list)
+    encs = defaultdict(list)  # (slab, encode schedule) -> GB/s
     combos = [(n, sc) for n in names for sc in a.scheds]
+    ecombos = [(n, w) for n in names for w in a.enc_scheds]
     for rd in range(a.rounds):
         rot = combos[(rd * 7) % len(combos):] + combos[:(rd * 7) % len(combos)]
         for n, sc in rot:
@@ -109,6 +111,12 @@ def run(a):
         E.set_schedule()
         for n in names:
             enc[n].append(ebytes / timed(slabs[n].encode, 2) / 1e9)
+        erot = ecombos[(rd * 5) % max(1, len(ecombos)):] + ecombos[:(rd * 5) % max(1, len(ecombos))]
+        for n, w in erot:  # the encode under each write-window / tile-order setting
+            base, _, rflag = w.partition("+")
+            E.set_schedule(**E.parse_schedule(window=base, remap="1" if rflag == "r" else None))
+            encs[(n, w)].append(ebytes / timed(slabs[n].encode, 2) / 1e9)
+        E.set_schedule()
         print(f"round {rd + 1}/{a.rounds} done", flush=True)
     E.set_schedule()
     med = {key: statistics.median(v) for key, v in rep.items()}
@@ -131,6 +139,20 @@ def run(a):
     if split_auto:
         sv = [med[("S", sc)] for sc in a.scheds]
         print("split slab: " + " ".join(f"{sc}={x:.1f}" for sc, x in zip(a.scheds, sv)))
+    if a.enc_scheds:
+        emed = {key: statistics.median(v) for key, v in encs.items()}
+        print(f"\nencode GB/s per slab under each encode schedule (window: auto | off | on | LOG2P,W; +r = per-XCD "
+              f"tile order), median of {a.rounds} rounds x 2 encodes")
+        print("slab " + " ".join(f"{w:>10s}" for w in a.enc_scheds))
+        for n in names:
+            print(f"{n:4s} " + " ".join(f"{emed[(n, w)]:10.1f}" for w in a.enc_scheds))
+        print("per encode schedule over the tiled slabs: worst / median / best")
+        erank = []
+        for w in a.enc_scheds:
+            v = sorted(emed[(n, w)] for n in tiled)
+            print(f"  {w:10s} {v[0]:7.1f} {statistics.median(v):7.1f} {v[-1]:7.1f}")
+            erank.append((v[0], w))
+        print(f"best encode schedule by worst tiled slab: {max(erank)[1]} ({max(erank)[0]:.1f} GB/s)")
 
 
 def _csv_rows(path):
@@ -205,6 +227,9 @@ if __name__ == "__main__":
     ap.add_argument("--split", type=int, default=1, help="1: also a split slab (the same-process yardstick)")
     ap.add_argument("--split-at", type=int, default=2, help="its position in the allocation order")
     ap.add_argument("--scheds", nargs="+", default=SCHEDS)
+    ap.add_argument("--enc-scheds", nargs="*", default=[],
+                    help="also time each slab's encode under these write-window settings (auto | off | on | "
+                         "LOG2P,W, '+r' = per-XCD tile order)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--seed", type=int, default=103)
