@@ -98,6 +98,7 @@ SIGNATURES = {
     "ecw_service_counters": (c_int, [c_int, POINTER(c_uint64)]),
     "ecw_set_schedule": (c_int, [POINTER(ecw_schedule)]),
     "ecw_host_alloc": (c_int, [c_int, c_size_t, POINTER(c_void_p), POINTER(c_int)]),
+    "ecw_host_alloc_node": (c_int, [c_int, c_int, c_size_t, POINTER(c_void_p), POINTER(c_int)]),
     "ecw_host_free": (c_int, [c_void_p]),
     "ecw_device_numa_node": (c_int, [c_int]),
     "ecw_get_schedule": (c_int, [POINTER(ecw_schedule)]),

@@ -419,19 +419,19 @@ def parse_schedule(xor: str | None = None, window: str | None = None, remap: str
 
 
 class PinnedHost:
-    """Host memory on the NUMA node of `device`'s PCIe root, pinned for DMA
-    (ecw_host_alloc): staging for the host-memory entry points that keeps
+    """Host memory on the NUMA node of `device`'s PCIe root (or on `node`),
+    pinned for DMA (ecw_host_alloc_node): staging for the host-memory entry points that keeps
     their copies at PCIe rate and off the inter-socket fabric. `.array` is a
     uint8 numpy view; `.numa_node` the node its pages were found on (-1:
     unknown). Freed by free() or when the object is collected."""
 
-    def __init__(self, nbytes: int, device: int = 0):
+    def __init__(self, nbytes: int, device: int = 0, node: int = -1):
         import weakref
 
-        p, node = c_void_p(), c_int(-1)
-        _check(lib.ecw_host_alloc(device, nbytes, byref(p), byref(node)), f"host_alloc({nbytes})")
+        p, got = c_void_p(), c_int(-1)
+        _check(lib.ecw_host_alloc_node(device, node, nbytes, byref(p), byref(got)), f"host_alloc({nbytes}, node {node})")
         self.ptr, self.nbytes, self.device = p.value, int(nbytes), device
-        self.numa_node = node.value
+        self.numa_node = got.value
         self.device_numa_node = lib.ecw_device_numa_node(device)
         raw = (ctypes.c_uint8 * self.nbytes).from_address(self.ptr)
         raw.owner = self  # views of `array` keep the allocation alive (freed when the last one goes)

@@ -1643,12 +1643,16 @@ extern "C++" int counters(int device, unsigned long long out[4]) {
 }  // namespace svc
 
 int ecw_host_alloc(int device, size_t bytes, void** out, int* numa_node) {
-  if (!out || bytes == 0 || device < 0) return ECW_EINVAL;
+  return ecw_host_alloc_node(device, -1, bytes, out, numa_node);
+}
+
+int ecw_host_alloc_node(int device, int node, size_t bytes, void** out, int* numa_node) {
+  if (!out || bytes == 0 || device < 0 || node < -1 || node >= 1024) return ECW_EINVAL;
   *out = nullptr;
   if (numa_node) *numa_node = -1;
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || device >= ndev) return ECW_EDEVICE;
-  const int node = device_numa_node(device);
+  if (node < 0) node = device_numa_node(device);
   const size_t n = (bytes + 4095) & ~static_cast<size_t>(4095);
   void* p = mmap(nullptr, n, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
   if (p == MAP_FAILED) return ECW_ENOMEM;

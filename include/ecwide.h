@@ -205,6 +205,10 @@ int ecw_repair(ecw_codec* codec, const uint8_t* const* blocks, int lost_block, u
  * -1 when unknown or spread). Free with ecw_host_free. No reference
  * counterpart (placement of the caller's buffers). ECW_EDEVICE without a GPU. */
 int ecw_host_alloc(int device, size_t bytes, void** out, int* numa_node);
+/* The same with the pages preferred on NUMA node `node` (-1: `device`'s node),
+ * registered for `device`: staging next to another socket's DRAM, e.g. where
+ * the files' page cache lives, or a local-versus-remote A/B. */
+int ecw_host_alloc_node(int device, int node, size_t bytes, void** out, int* numa_node);
 int ecw_host_free(void* ptr);
 /* NUMA node of `device` (-1 when unknown or no such device). */
 int ecw_device_numa_node(int device);

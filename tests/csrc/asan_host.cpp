@@ -311,6 +311,8 @@ static void schedule_and_host() {
   CHECK(ecw_host_free(nullptr) == ECW_OK);
   CHECK(ecw_host_free(&node) == ECW_EINVAL);
   CHECK(ecw_device_numa_node(0) == -1);
+  CHECK(ecw_host_alloc_node(0, 5000, 4096, &p, &node) == ECW_EINVAL);
+  CHECK(ecw_host_alloc_node(0, 0, 4096, &p, &node) == ECW_EDEVICE && p == nullptr);
 }
 
 int main() {

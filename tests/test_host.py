@@ -273,5 +273,9 @@ def test_host_alloc_without_gpu_fails_cleanly():
     assert _lib.lib.ecw_host_free(None) == 0
     assert _lib.lib.ecw_host_free(c_void_p(4096)) == -1  # not ours
     assert _lib.lib.ecw_device_numa_node(0) == -1
+    assert _lib.lib.ecw_host_alloc_node(0, 2000, 4096, byref(p), None) == -1  # node out of range
+    assert _lib.lib.ecw_host_alloc_node(0, -1, 4096, byref(p), byref(node)) == -3
     with pytest.raises(E.EcwError):
         E.PinnedHost(4096)
+    with pytest.raises(E.EcwError):
+        E.PinnedHost(4096, node=0)
