@@ -48,6 +48,28 @@ __device__ __forceinline__ uint8_t* xdst(const XorPtr& a, int) { return a.dst; }
 __device__ __forceinline__ uint8_t* xdst(const XorSlab& a, int s) { return a.out + s * a.ostride; }
 __device__ __forceinline__ uint8_t* xdst(const XorSplit& a, int s) { return a.out + s * a.ostride; }
 
+// Pairs of consecutive units of a split slab taken as one unit of 4 tiles, so
+// that K = 4 can skew over the tiled slab's 2-tile (8 KiB) pieces: tile q of
+// pair p is tile q % 2 of unit 2p + q / 2 (launch_xor_range). The units of a
+// source are sstride (data) or psstride (parity) apart, the outputs ostride.
+struct XorSplitPair {
+  XorSplit a;
+};
+template <class Args>
+struct is_pair : std::false_type {};
+template <>
+struct is_pair<XorSplitPair> : std::true_type {};
+__device__ __forceinline__ const uint8_t* xsrc(const XorSplitPair& p, int s, int i) { return xsrc(p.a, 2 * s, i); }
+__device__ __forceinline__ uint8_t* xdst(const XorSplitPair& p, int s) { return xdst(p.a, 2 * s); }
+// byte offset of tile q of a pair from its first tile, in source i / the output
+__device__ __forceinline__ uint64_t pair_src_off(const XorSplitPair& p, int i, int q) {
+  return static_cast<uint64_t>(q >> 1) * (i < p.a.ndata ? p.a.sstride : p.a.psstride) +
+         static_cast<uint64_t>(q & 1) * kTileBytes;
+}
+__device__ __forceinline__ uint64_t pair_dst_off(const XorSplitPair& p, int q) {
+  return static_cast<uint64_t>(q >> 1) * p.a.ostride + static_cast<uint64_t>(q & 1) * kTileBytes;
+}
+
 // Loads and stores of the XOR reduce are nontemporal (+4-6 % at 4-64 MiB
 // blocks; a straight stream, every byte touched once).
 constexpr bool kXorNt = true;
@@ -137,7 +159,10 @@ __device__ __forceinline__ void xor_tiles_fixed(const Args& a, const XorGeom& g,
   // otherwise pull the first XORs up between the first loads: vmcnt(0) after two)
 #pragma unroll
   for (int t = 0; t < T; ++t) {
-    v[t] = ld16<TAIL, kXorNt>(sp[t % N], col + ((t / N + t % N) % K) * kTileBytes, len);
+    if constexpr (is_pair<Args>::value)
+      v[t] = ld16<TAIL, kXorNt>(sp[t % N] + pair_src_off(a, t % N, (t / N + t % N) % K), col, len);
+    else
+      v[t] = ld16<TAIL, kXorNt>(sp[t % N], col + ((t / N + t % N) % K) * kTileBytes, len);
     __builtin_amdgcn_sched_barrier(0);
     if (t >= W - 1) {
       const int u = t - W + 1;
@@ -154,7 +179,12 @@ __device__ __forceinline__ void xor_tiles_fixed(const Args& a, const XorGeom& g,
   xor_write_window(sc.wmask, sc.wwidth);
   uint8_t* d = xdst(a, s);
 #pragma unroll
-  for (int q = 0; q < K; ++q) st16<TAIL, kXorNt>(d, col + q * kTileBytes, len, acc[q]);
+  for (int q = 0; q < K; ++q) {
+    if constexpr (is_pair<Args>::value)
+      st16<TAIL, kXorNt>(d + pair_dst_off(a, q), col, len, acc[q]);
+    else
+      st16<TAIL, kXorNt>(d, col + q * kTileBytes, len, acc[q]);
+  }
 }
 
 // Groups of K column tiles, numbered stripe-major (order 0: group = stripe *
@@ -205,6 +235,7 @@ inline XorSplit offset_stripes(const XorSplit& a, int s0) {
   o.out += static_cast<uint64_t>(s0) * a.ostride;
   return o;
 }
+inline XorSplitPair offset_stripes(const XorSplitPair& p, int s0) { return XorSplitPair{offset_stripes(p.a, 2 * s0)}; }
 inline XorTab offset_stripes(const XorTab& a, int s0) {
   XorTab o = a;
   o.src += static_cast<uint64_t>(s0) * a.n;
@@ -312,6 +343,13 @@ hipError_t launch_xor_range(const Args& a, const XorGeom& g, hipStream_t s) {
     static_assert(sizeof(kXorSkews) / sizeof(kXorSkews[0]) == 3 && kXorSkews[1] == 2 && kXorSkews[2] == 4,
                   "the skews instantiated here are the ones ecw_set_schedule accepts");
     static_assert(kXorSkewWhole == 4 || kXorSkewWhole == 2 || kXorSkewWhole == 1, "a built skew");
+    if constexpr (std::is_same<Args, XorSplit>::value) {
+      // K = 4 over 2-tile units (the tiled slab's 8 KiB pieces): pairs of units
+      if (c.skew == 4 && g.len == 2 * kTileBytes && g.stripes % 2 == 0) {
+        const XorGeom gp{4 * kTileBytes, 4, g.stripes / 2, g.n};
+        return launch_xor_skew<4>(XorSplitPair{a}, gp, c, s);
+      }
+    }
     if (c.skew == 4) return launch_xor_skew<4>(a, g, c, s);
     if (c.skew == 2) return launch_xor_skew<2>(a, g, c, s);
     return launch_xor_skew<1>(a, g, c, s);

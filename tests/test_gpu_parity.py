@@ -600,6 +600,40 @@ def test_xor_schedules_same_bytes(E, torch, orc, schedule, sched):
                     (layout, lost, s)
 
 
+@pytest.mark.parametrize("sched", [None, "1,0", "2,0", "2,0,11,64", "2,1,11,64", "4,0", "4,1", "4,0,11,64"])
+@pytest.mark.parametrize("pieces", [8, 7])
+def test_tiled_repair_schedules_same_bytes(E, torch, orc, schedule, sched, pieces):
+    """The tiled slab's repair (8 KiB units = 2 column tiles; ecw_xor.hpp) under
+    every schedule -- K = 4 takes pairs of units (XorSplitPair) when the unit
+    count is even and falls back to ragged groups when it is odd -- rebuilds
+    every lost D and L block exactly, with the default (K = 2 + window at
+    >= 8192 tiles) among them."""
+    E.set_schedule(**E.parse_schedule(xor=sched))
+    k, m, r, S = 40, 2, 27, 3
+    B = pieces * 8192  # 3 x 8 = 24 units (pairs) or 3 x 7 = 21 (odd: no pairing)
+    c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False)
+    slab = E.StripeSlab(c, stripes=S, block_bytes=B, layout="tiled", chunk=8192)
+    slab.fill_random(seed=57)
+    slab.encode()
+    out = torch.full((S * B,), 0x33, dtype=torch.uint8, device="cuda")
+    for lost in (0, 26, 27, k + m, k + m + 1):
+        slab.repair(lost, out)
+        torch.cuda.synchronize()
+        for s_ in range(S):
+            assert torch.equal(out[s_ * B:(s_ + 1) * B], slab.block(s_, lost)), (sched, pieces, lost, s_)
+    # the bench's unit count with the window's launch floor reached (>= 8192 tiles)
+    Bb, Sb = 4 << 20, 16  # 16 stripes x 512 units x 2 tiles = 16384 tiles
+    cb = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(128, 3, 27, Bb), 1, False)
+    big = E.StripeSlab(cb, stripes=Sb, block_bytes=Bb, layout="tiled", chunk=8192)
+    big.fill_random(seed=58)
+    big.encode()
+    outb = torch.empty(Sb * Bb, dtype=torch.uint8, device="cuda")
+    big.repair(0, outb)
+    torch.cuda.synchronize()
+    for s_ in (0, Sb - 1):
+        assert torch.equal(outb[s_ * Bb:(s_ + 1) * Bb], big.block(s_, 0)), (sched, s_)
+
+
 def test_block_batch_encode_repair(E, torch, orc):
     """BlockBatch: a batch of stripes of separately allocated blocks, encoded and
     every D and L block repaired through device pointer tables, one launch each."""
