@@ -292,9 +292,16 @@ struct XorChoice {
 //    own default in the same process. K = 4 + window was the worst (6090 / 6167:
 //    a 2-tile unit is a ragged group of 4, reduced tile by tile), K = 2 without
 //    the window no better than K = 1, a 2^10 / 32 window between (6320 / 6340);
+//  * ... and, later in round 5, K = 4 over PAIRS of those units (XorSplitPair:
+//    the split / tiled slab's addressing, an even unit count) + the window beat
+//    K = 2 + window on the worst slab in both processes: 6541 / 6373 against
+//    6426 / 6318 GB/s (median 6578 / 6518 against 6487 / 6473; 0.998 / 0.995 of
+//    the split slab's default; profiles/r05f_pair_placement_1/2.log). Units that
+//    cannot be paired (odd count, pointer tables) keep K = 2 + window;
 //  * the XOR keeps the dispatch tile order (the per-XCD order: -0.4..-5 %,
 //    profiles/r04_remap_*.log).
-inline XorChoice xor_choice(const XorGeom& g) {
+// `pairable`: the launch can take pairs of 2-tile units (launch_xor_range).
+inline XorChoice xor_choice(const XorGeom& g, bool pairable) {
   constexpr uint64_t group = static_cast<uint64_t>(kXorSkewWhole) * kTileBytes;
   const uint64_t tiles = static_cast<uint64_t>(g.stripes) * g.tiles;
   const bool whole = g.len >= 65536 || (g.len >= group && g.len % group == 0);
@@ -302,7 +309,7 @@ inline XorChoice xor_choice(const XorGeom& g) {
   // for the window
   const bool pair = !whole && g.len == 2 * kTileBytes && g.n >= 8 && tiles >= 8192;
   const Schedule sc = current_schedule();
-  XorChoice c{whole ? kXorSkewWhole : pair ? 2 : 1, 0, 11, 0, 0};
+  XorChoice c{whole ? kXorSkewWhole : pair ? (pairable ? 4 : 2) : 1, 0, 11, 0, 0};
   if ((whole || pair) && g.n >= 8 && tiles >= 8192) c.wwidth = 64;
   if (sc.xor_skew > 0) c.skew = sc.xor_skew;
   if (sc.xor_order >= 0) c.order = static_cast<uint32_t>(sc.xor_order);
@@ -339,13 +346,14 @@ hipError_t launch_xor_range(const Args& a, const XorGeom& g, hipStream_t s) {
   const dim3 grid(grid_for(total, kGridPerCuXor)), block(kBlock);
   const FastDiv per = make_fastdiv(static_cast<uint32_t>(g.tiles));
   if (g.n <= kXorFixedMax) {
-    const XorChoice c = xor_choice(g);
+    const bool pairable = std::is_same<Args, XorSplit>::value && g.stripes % 2 == 0;
+    const XorChoice c = xor_choice(g, pairable);
     static_assert(sizeof(kXorSkews) / sizeof(kXorSkews[0]) == 3 && kXorSkews[1] == 2 && kXorSkews[2] == 4,
                   "the skews instantiated here are the ones ecw_set_schedule accepts");
     static_assert(kXorSkewWhole == 4 || kXorSkewWhole == 2 || kXorSkewWhole == 1, "a built skew");
     if constexpr (std::is_same<Args, XorSplit>::value) {
       // K = 4 over 2-tile units (the tiled slab's 8 KiB pieces): pairs of units
-      if (c.skew == 4 && g.len == 2 * kTileBytes && g.stripes % 2 == 0) {
+      if (c.skew == 4 && g.len == 2 * kTileBytes && pairable) {
         const XorGeom gp{4 * kTileBytes, 4, g.stripes / 2, g.n};
         return launch_xor_skew<4>(XorSplitPair{a}, gp, c, s);
       }
