@@ -16,6 +16,8 @@
 //     (Compiled from C++, any store in the row loop makes LLVM's waitcnt pass
 //     fall back to vmcnt(0) at the loop head, i.e. drain the ring every two
 //     rows; that cost ~4 % of encode time at k=128.)
+//     With the write window on (whole-block layouts) the <= 4-row tile keeps a
+//     third slot in flight (ECW_TILE_ASM3, vmcnt(2); ecw_tuning.hpp ECW_ASM_RING3).
 //   * per row: the 32 table lookups are issued in two alternating sets of 8
 //     (ds_read_b32 into the address register itself), each set folded into
 //     the packed accumulators with v_bitop3 (xor3) while the next is in
@@ -344,7 +346,10 @@
   ECW_ROW_DRAIN                                                             \
   ECW_WRITE_WINDOW                                                          \
   END                                                                       \
-  /* global rows: byte l of the packed accumulators -> output row l */      \
+  ECW_GLOBAL_ROWS(MODE)
+
+// global rows: byte l of the packed accumulators -> output row l (v[36:39])
+#define ECW_GLOBAL_ROWS(MODE)                                                    \
   ECW_GPTR_INIT_##MODE                                                      \
   "s_mov_b32 s56, 0\n\t"                                                    \
   "30:\n\t"                                                                 \
@@ -377,6 +382,100 @@
   "s_add_u32 s56, s56, 1\n\t"                                               \
   "s_branch 30b\n\t"                                                        \
   "31:"
+
+// Three-slot ring (kAsmRing3, k >= 3): slot C is v[36:39], the output-row
+// registers, which the row loop does not use; rows j, j+1, j+2 are in flight
+// and each consumption waits with vmcnt(2). Same rows, boundaries and stores
+// as ECW_TILE_ASM; 1 KiB more read in flight per wave at no register cost.
+#define ECW_LOAD_C "global_load_dwordx4 v[36:39], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
+#define ECW_ROW_C(XL) ECW_ROW("v36", "v37", "v38", "v39", XL)
+#define ECW_ROW_PRE_C(XL) ECW_ROW_PRE("v36", "v37", "v38", "v39", XL)
+#define ECW_TILE_ASM3(BND, XL, END, MODE)                                          \
+  "v_mov_b32 v40, %[col]\n\t"                                               \
+  "v_mov_b32 v33, 0x3c3c3c3c\n\t"                                           \
+  "s_mov_b32 s50, 0x0c0c0400\n\t"                                           \
+  "s_mov_b32 s51, 0x0c0c0401\n\t"                                           \
+  "s_mov_b32 s52, 0x0c0c0402\n\t"                                           \
+  "s_mov_b32 s53, 0x0c0c0403\n\t"                                           \
+  ECW_ROWPTR_INIT_##MODE                                                    \
+  ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
+  ECW_LOAD_B ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
+  ECW_LOAD_C ECW_NEXTROW_##MODE                                             \
+  "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
+  "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
+  "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
+  "v_mov_b32 v24, 0\n\tv_mov_b32 v25, 0\n\tv_mov_b32 v26, 0\n\tv_mov_b32 v27, 0\n\t" \
+  "v_mov_b32 v28, 0\n\tv_mov_b32 v29, 0\n\tv_mov_b32 v30, 0\n\tv_mov_b32 v31, 0\n\t" \
+  ECW_ROW_YZERO                                                             \
+  "s_mov_b32 s44, 0\n\t"                                                    \
+  "s_mov_b32 s59, 0\n\t"                                                    \
+  "s_mov_b32 s46, %[lds]\n\t"                                               \
+  ECW_LPTR_INIT_##MODE                                                      \
+  "s_min_u32 s45, %[r], %[k]\n\t"                                           \
+  /* main loop: rows j..j+2 while rows j+3..j+5 exist */                    \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 5\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_C(XL), ECW_LOAD_C, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  /* 3, 4 or 5 rows left (k - j); slots A, B, C hold rows j, j+1, j+2 */    \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc1 12f\n\t"                                                  \
+  "s_cmp_eq_u32 s49, 4\n\t"                                                 \
+  "s_cbranch_scc1 14f\n\t"                                                  \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_B(XL), ECW_LOAD_B, , BND)                     \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_ROW_C(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_A(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW_ROW_B(XL) BND                                                         \
+  "s_branch 13f\n\t"                                                        \
+  "14:\n\t"                                                                 \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                     \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_ROW_B(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_C(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW_ROW_A(XL) BND                                                         \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  ECW_ROW_A(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW_ROW_B(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW_ROW_C(XL) BND                                                         \
+  "13:\n\t"                                                                 \
+  ECW_ROW_DRAIN                                                             \
+  ECW_WRITE_WINDOW                                                          \
+  END                                                                       \
+  ECW_GLOBAL_ROWS(MODE)
 
 #define ECW_TILE_OPERANDS                                                          \
   : : [row0] "s"(row0), [lrow0] "s"(lrow0), [grow0] "s"(grow0), [bslo] "s"(bslo), \
@@ -935,16 +1034,16 @@ namespace {
 // mode always stores its zero L blocks there); TAB:
 // block pointers come from pointer tables (see ECW_ROWPTR_INIT_TAB). Requires
 // k >= 2, a full tile (every lane's 16 bytes in range) and exec = all lanes.
-#define ECW_TILE_CALL(MODE)                                                              \
+#define ECW_TILE_CALL(TILE, MODE)                                                           \
   if constexpr (LOCAL == kLocalNone) {                                                   \
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW_TILE_OPERANDS);           \
+    asm volatile(TILE(ECW_BOUNDARY_NONE, 0, , MODE) ECW_TILE_OPERANDS);           \
   } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_PARK, 1, ECW_STORE_PARKED(MODE), MODE)        \
+    asm volatile(TILE(ECW_BOUNDARY_PARK, 1, ECW_STORE_PARKED(MODE), MODE)        \
                      ECW_TILE_OPERANDS_PARK);                                            \
   } else if constexpr (LOCAL == kLocalXor) {                                             \
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW_TILE_OPERANDS);       \
+    asm volatile(TILE(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW_TILE_OPERANDS);       \
   } else {                                                                               \
-    asm volatile(ECW_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)          \
+    asm volatile(TILE(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)          \
                      ECW_TILE_OPERANDS);                                                 \
   }
 
@@ -982,6 +1081,7 @@ __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lr
                                                 uint32_t col, uint32_t wmask, uint32_t ww) {
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
   const uint32_t pbslo = static_cast<uint32_t>(pbstride), pbshi = static_cast<uint32_t>(pbstride >> 32);
+  const bool ring3 = k >= 3 && (kAsmRing3 == 2 || (kAsmRing3 == 1 && ww != 0));  // uniform: a scalar branch
   if constexpr (NW == 4) {
     if constexpr (TAB) {
       ECW4_TILE_CALL(TAB)
@@ -995,9 +1095,17 @@ __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lr
       ECW2_TILE_CALL(SLAB)
     }
   } else if constexpr (TAB) {
-    ECW_TILE_CALL(TAB)
+    if (ring3) {
+      ECW_TILE_CALL(ECW_TILE_ASM3, TAB)
+    } else {
+      ECW_TILE_CALL(ECW_TILE_ASM, TAB)
+    }
   } else {
-    ECW_TILE_CALL(SLAB)
+    if (ring3) {
+      ECW_TILE_CALL(ECW_TILE_ASM3, SLAB)
+    } else {
+      ECW_TILE_CALL(ECW_TILE_ASM, SLAB)
+    }
   }
 }
 

@@ -40,6 +40,13 @@
 // (+3-5 %; +32 % at k = 200, profiles/r03_tpb_ab.log)
 #define ECW_ASM_TPB4 2
 #endif
+#ifndef ECW_ASM_RING3
+// <= 4-row asm tile: when it keeps 3 rows in flight per wave instead of 2 (slot C
+// in v[36:39], no register cost). 0 never, 1 with the write window (the
+// whole-block layouts at k >= 64: +0.8..1.8 % encode), 2 always (tiled slab
+// -0.5..+0.5 % at k = 128, -1.2..-2.1 % at k = 32; profiles/r05h_*, r05i_*)
+#define ECW_ASM_RING3 1
+#endif
 #ifndef ECW_ASM_TPB1
 #define ECW_ASM_TPB1 1  // <= 4 rows (2: tiled +-0, block slab -1.2 %, profiles/r03_tpb1_ab.log)
 #endif
@@ -84,6 +91,8 @@
 namespace ecw {
 constexpr int kPrefetchEnc = ECW_PREFETCH_ENC;
 constexpr int kPrefetchEncAsmTail = 2;  // the asm launches' ragged-tail kernel
+constexpr int kAsmRing3 = ECW_ASM_RING3;
+static_assert(kAsmRing3 >= 0 && kAsmRing3 <= 2, "ECW_ASM_RING3: 0, 1 or 2");
 constexpr uint64_t kGridPerCu = ECW_GRID_PER_CU;
 constexpr uint64_t kGridPerCuXor = ECW_GRID_PER_CU_XOR;
 constexpr int kPrefetchXor = ECW_PREFETCH_XOR;

@@ -354,6 +354,12 @@ def test_ticket_launches_on_per_thread_streams(E, torch, orc):
     (24, 2, 3, "xor", "split"),       # 8 groups: mid-tile local stores
     (16, 3, 4, "literal", "blocks"),  # zero L blocks
     (32, 3, 11, "xor", "ptr"),        # device pointer tables
+    (3, 2, 2, "xor", "blocks"),       # window on = the three-slot ring: its 3-row tail only
+    (4, 3, 4, "xor", "ptr"),          # 4-row tail, pointer tables
+    (5, 1, 2, "xor", "split"),        # 5-row tail, 3 groups (parked locals)
+    (7, 2, 1, "xor", "split"),        # main loop once + 4-row tail, 7 groups (mid-tile local stores)
+    (9, 3, 3, "literal", "blocks"),   # main loop once + 3-row tail, zero L blocks
+    (10, 4, 10, "xor", "blocks"),     # main loop once + 4-row tail
 ])
 def test_write_window_same_bytes(E, torch, orc, schedule, k, m, r, local, layout):
     """The write window (ecw_kernels.hip set_schedule; ecw_set_schedule's
@@ -361,7 +367,9 @@ def test_write_window_same_bytes(E, torch, orc, schedule, k, m, r, local, layout
     parity stores: encodes with it forced off, on, and at another period give
     identical parities, equal to the oracle on a column window, and the default
     choice ('auto': whole-block slabs and pointer modes at k >= 64, <= 4 global rows, blocks >= 64 KiB,
-    >= 8192 tiles) is one of them."""
+    >= 8192 tiles) is one of them. With the window on, the <= 4-row tile keeps
+    three rows in flight (ECW_TILE_ASM3): k = 3, 4, 5, 9, 10 reach each tail of
+    that ring."""
     B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles
     c = E.NativeCodec.getClCodec(E.CodingScheme.getClScheme(k, m, r, B), 1, False, local_mode=local)
     np_ = c.parityNum

@@ -108,7 +108,7 @@ def main():
     if a.check:
         assert libs[0][1].ecw_encode_batch_dev(libs[0][2], c_void_p(buf.data_ptr()), bstride, sstride, S, B, stream) == 0
         torch.cuda.synchronize()
-        ref = buf[(k) * bstride:(k) * bstride + B].clone()
+        ref = torch.stack([buf[s_ * sstride + k * bstride:s_ * sstride + nblk * bstride] for s_ in range(S)]).clone()
     if a.ptr:
         base = buf.data_ptr()
         dptrs = [(c_void_p * k)(*[base + s_ * sstride + (k - 1 - j) * bstride for j in range(k)]) for s_ in range(S)]
@@ -153,8 +153,8 @@ def main():
             res[name][0].append(enc_bytes * a.iters / (e[0].elapsed_time(e[1]) * 1e-3) / 1e9)
             if rep_iters:
                 res[name][1].append(rep_bytes * rep_iters / (max(e[1].elapsed_time(e[2]), 1e-6) * 1e-3) / 1e9)
-            if ref is not None and "ablate" not in name:
-                got = buf[(k) * bstride:(k) * bstride + B]
+            if ref is not None and "ablate" not in name:  # every parity block of every stripe (pads included)
+                got = torch.stack([buf[s_ * sstride + k * bstride:s_ * sstride + nblk * bstride] for s_ in range(S)])
                 if not torch.equal(got, ref):
                     print(f"  !! {name}: parity differs from {libs[0][0]}")
     print(f"{a.code}(k={k},r={r},m={m}) B={B} x{S} stripes pad={a.pad}; GB/s median (min..max) over {a.rounds} rounds")

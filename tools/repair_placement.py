@@ -14,9 +14,13 @@ slow on a bad one is what the driver's box sees.
   python tools/repair_placement.py [--slabs 5] [--stripes 4] [--rounds 4] [--scheds auto 1,0 2,0,11,64 ...]
   rocprofv3 --pmc ... -- python3 tools/repair_placement.py --pmc-reps 3 ...   (fixed dispatch order)
   python tools/repair_placement.py --summarize <counter_collection.csv> [same --slabs/--scheds/--pmc-reps]
+  python tools/repair_placement.py --scheds auto --enc-libs build/variants/ring3.so ...   (encode builds A/B)
 
 Schedules are "K,ORDER[,LOG2P,W]" (ecwide_amd.parse_schedule; no window unless
-given) or "auto" (the library's own choice).
+given) or "auto" (the library's own choice). --enc-libs times every slab's
+encode through other builds of the library too (tools/variants.py: compile-time
+tile changes), on the same slabs in the same rounds, after checking that each
+build writes the same parity bytes as the package's own.
 """
 import argparse
 import csv
@@ -57,6 +61,34 @@ def run(a):
         sl.encode()
     torch.cuda.synchronize()
     print("allocation order " + " ".join(f"{n}@0x{slabs[n].buf.data_ptr():x}" for n in order), flush=True)
+    elibs = []  # (name, encode fn per slab) for each extra build of the library
+    if a.enc_libs:
+        from ctypes import byref, c_void_p
+
+        from ecwide_amd import _lib
+        st = c_void_p(torch.cuda.current_stream().cuda_stream)
+        for path in a.enc_libs:
+            L = _lib.load(path, strict=False)
+            sch = _lib.ecw_scheme()
+            assert L.ecw_scheme_init(byref(sch), b"C", k, m, r, B) == 0
+            h = c_void_p()
+            assert L.ecw_codec_create(byref(sch), 1, 0, 0, 0, byref(h)) == 0
+
+            def enc(sl, L=L, h=h):
+                n_, len_ = (sl.units, sl.chunk) if sl.layout == "tiled" else (sl.stripes, sl.len)
+                assert L.ecw_encode_batch_split_dev(h, *sl._split_args(), n_, len_, st) == 0
+            elibs.append((os.path.basename(path).rsplit(".", 1)[0], enc))
+        np_ = c.parityNum
+        for n, sl in slabs.items():  # same parity bytes as the package's build, every slab
+            want = [sl.block(s, k + i).clone() for s in (0, S - 1) for i in range(np_)]
+            for name, enc in elibs:
+                sl.buf[sl.off + sl.parity_offset:].zero_()  # the parity region ends the slab's buffer
+                enc(sl)
+                torch.cuda.synchronize()
+                got = [sl.block(s, k + i) for s in (0, S - 1) for i in range(np_)]
+                if not all(torch.equal(x, y) for x, y in zip(got, want)):
+                    raise SystemExit(f"slab {n}: build {name} writes other parity bytes")
+        print(f"every slab's parity identical under {len(elibs)} other build(s)", flush=True)
     rbytes = slabs[order[0]].repair_bytes(0)
     ebytes = slabs[order[0]].encode_bytes()
     names = list(slabs)
@@ -102,7 +134,8 @@ def run(a):
     enc = defaultdict(list)
     encs = defaultdict(list)  # (slab, encode schedule) -> GB/s
     combos = [(n, sc) for n in names for sc in a.scheds]
-    ecombos = [(n, w) for n in names for w in a.enc_scheds]
+    ecombos = [(n, w) for n in names for w in a.enc_scheds] + [(n, "lib:" + nm) for n in names for nm, _ in elibs]
+    efn = dict(elibs)
     for rd in range(a.rounds):
         rot = combos[(rd * 7) % len(combos):] + combos[:(rd * 7) % len(combos)]
         for n, sc in rot:
@@ -113,6 +146,10 @@ def run(a):
             enc[n].append(ebytes / timed(slabs[n].encode, 2) / 1e9)
         erot = ecombos[(rd * 5) % max(1, len(ecombos)):] + ecombos[:(rd * 5) % max(1, len(ecombos))]
         for n, w in erot:  # the encode under each write-window / tile-order setting
+            if w.startswith("lib:"):
+                E.set_schedule()
+                encs[(n, w)].append(ebytes / timed(lambda: efn[w[4:]](slabs[n]), 2) / 1e9)
+                continue
             base, _, rflag = w.partition("+")
             E.set_schedule(**E.parse_schedule(window=base, remap="1" if rflag == "r" else None))
             encs[(n, w)].append(ebytes / timed(slabs[n].encode, 2) / 1e9)
@@ -139,16 +176,17 @@ def run(a):
     if split_auto:
         sv = [med[("S", sc)] for sc in a.scheds]
         print("split slab: " + " ".join(f"{sc}={x:.1f}" for sc, x in zip(a.scheds, sv)))
-    if a.enc_scheds:
+    ecols = a.enc_scheds + ["lib:" + nm for nm, _ in elibs]
+    if ecols:
         emed = {key: statistics.median(v) for key, v in encs.items()}
         print(f"\nencode GB/s per slab under each encode schedule (window: auto | off | on | LOG2P,W; +r = per-XCD "
               f"tile order), median of {a.rounds} rounds x 2 encodes")
-        print("slab " + " ".join(f"{w:>10s}" for w in a.enc_scheds))
+        print("slab " + " ".join(f"{w:>10s}" for w in ecols))
         for n in names:
-            print(f"{n:4s} " + " ".join(f"{emed[(n, w)]:10.1f}" for w in a.enc_scheds))
+            print(f"{n:4s} " + " ".join(f"{emed[(n, w)]:10.1f}" for w in ecols))
         print("per encode schedule over the tiled slabs: worst / median / best")
         erank = []
-        for w in a.enc_scheds:
+        for w in ecols:
             v = sorted(emed[(n, w)] for n in tiled)
             print(f"  {w:10s} {v[0]:7.1f} {statistics.median(v):7.1f} {v[-1]:7.1f}")
             erank.append((v[0], w))
@@ -230,6 +268,8 @@ if __name__ == "__main__":
     ap.add_argument("--enc-scheds", nargs="*", default=[],
                     help="also time each slab's encode under these write-window settings (auto | off | on | "
                          "LOG2P,W, '+r' = per-XCD tile order)")
+    ap.add_argument("--enc-libs", nargs="*", default=[],
+                    help="also time each slab's encode through these builds of libecwide.so (tools/variants.py)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=4)
     ap.add_argument("--seed", type=int, default=103)
