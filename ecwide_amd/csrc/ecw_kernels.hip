@@ -514,15 +514,22 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 // -4 %, pointer mode k=32 -8 %, k=8 -47 %; k=64 +5.5 %, k=96 +4.2 %, k=200 +7 %,
 // RS(128, 3) +3.1 %; profiles/r02_encode_write_window_k*.log), so only k >= 64
 // uses it, and not the 5-8-row tile (4 waves per SIMD: -1.2 %).
+// Units of 8-64 KiB (the tiled slab's 8 KiB pieces at k = 128) take it too since
+// round 5, with a 32-tick width: the window (and the three-slot ring it brings,
+// ecw_encode_asm.hpp) narrows the encode's placement band from 5994-6391 to
+// 6229-6304 GB/s over five slabs side by side, worst slab +0.2..4.5 % in six
+// processes, median -1.4..+1.7 % (profiles/r05k_*, r05l_*, r05m_*: judged by the
+// worst slab, as the repair's schedule).
 // ecw_set_schedule (enc_window_*) overrides the choice for the process.
 inline bool window_shape(const EncodeGeom& g) {
-  return g.k >= 64 && g.nrows <= 4 && g.len >= 65536 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
+  return g.k >= 64 && g.nrows <= 4 && g.len >= 8192 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
 }
+inline uint32_t window_width(const EncodeGeom& g) { return g.len >= 65536 ? 64u : 32u; }
 // Slabs of whole blocks: the block slab (parity rows after each stripe's data
 // rows) since round 2; the split slab (parities in a region of their own)
 // since round 4, interleaved in one process: 5557 -> 6350 and 5846 -> 6285 GB/s
 // (profiles/r04b_repair_ab_*.log; round 2 had measured +5.0 / -2.4 % on two
-// boxes). The tiled slab's 8 KiB units are below window_shape's 64 KiB.
+// boxes); the tiled slab's 8 KiB units since round 5 (above).
 inline bool window_auto(const SlabRows&, const EncodeGeom& g) { return window_shape(g); }
 inline bool window_auto(const PtrRows&, const EncodeGeom& g) { return window_shape(g); }
 inline bool window_auto(const PtrTabRows&, const EncodeGeom& g) { return window_shape(g); }
@@ -549,7 +556,7 @@ void set_schedule(const Rows& rows, EncodeGeom& g) {
   const bool on = sc.enc_width >= 0 ? sc.enc_width > 0 : window_auto(rows, g);
   const uint32_t log2p = sc.enc_log2p >= 0 ? static_cast<uint32_t>(sc.enc_log2p) : 11u;
   g.wmask = (1u << log2p) - 1;
-  g.wwidth = on ? (sc.enc_width > 0 ? static_cast<uint32_t>(sc.enc_width) : 64u) : 0u;
+  g.wwidth = on ? (sc.enc_width > 0 ? static_cast<uint32_t>(sc.enc_width) : window_width(g)) : 0u;
   g.remap = sc.xcd_remap >= 0 ? static_cast<uint32_t>(sc.xcd_remap) : remap_auto(rows);
 }
 
