@@ -521,9 +521,17 @@ hipError_t launch_encode_asm(const Rows& rows, const EncodeGeom& g, const uint4*
 // processes, median -1.4..+1.7 % (profiles/r05k_*, r05l_*, r05m_*: judged by the
 // worst slab, as the repair's schedule).
 // ecw_set_schedule (enc_window_*) overrides the choice for the process.
+// Stripes of 24-63 data blocks take it too since round 5, at half the period
+// (2^10 ticks): their tiles read a quarter of k = 128's rows, and at 2^11 the
+// generations cost more than the window saves (the -4 / -8 % above), while at
+// 2^10 the encode gains +4..6 % at k = 32 on the tiled, split and block slabs
+// (worst slab and median) and +4.5 % over pointer tables, +3.6 % at k = 24,
+// +1.5..2.3 % at k = 48; k = 16 loses 1 % (profiles/r05p_*, r05q_*, r05r_*);
+// 2^9 gains nothing anywhere.
 inline bool window_shape(const EncodeGeom& g) {
-  return g.k >= 64 && g.nrows <= 4 && g.len >= 8192 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
+  return g.k >= 24 && g.nrows <= 4 && g.len >= 8192 && static_cast<uint64_t>(g.stripes) * g.tiles >= 8192;
 }
+inline uint32_t window_log2p(const EncodeGeom& g) { return g.k >= 64 ? 11u : 10u; }
 inline uint32_t window_width(const EncodeGeom& g) { return g.len >= 65536 ? 64u : 32u; }
 // Slabs of whole blocks: the block slab (parity rows after each stripe's data
 // rows) since round 2; the split slab (parities in a region of their own)
@@ -554,7 +562,7 @@ template <class Rows>
 void set_schedule(const Rows& rows, EncodeGeom& g) {
   const Schedule sc = current_schedule();
   const bool on = sc.enc_width >= 0 ? sc.enc_width > 0 : window_auto(rows, g);
-  const uint32_t log2p = sc.enc_log2p >= 0 ? static_cast<uint32_t>(sc.enc_log2p) : 11u;
+  const uint32_t log2p = sc.enc_log2p >= 0 ? static_cast<uint32_t>(sc.enc_log2p) : window_log2p(g);
   g.wmask = (1u << log2p) - 1;
   g.wwidth = on ? (sc.enc_width > 0 ? static_cast<uint32_t>(sc.enc_width) : window_width(g)) : 0u;
   g.remap = sc.xcd_remap >= 0 ? static_cast<uint32_t>(sc.xcd_remap) : remap_auto(rows);

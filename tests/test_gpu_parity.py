@@ -351,6 +351,7 @@ def test_ticket_launches_on_per_thread_streams(E, torch, orc):
 @pytest.mark.parametrize("k,m,r,local,layout", [
     (128, 3, 27, "xor", "blocks"),    # parked locals (the bench shape's tile); auto = on
     (128, 3, 27, "xor", "tiled"),     # the bench's 8 KiB pieces (4096 units x 2 tiles); auto = on, width 32
+    (32, 3, 11, "xor", "tiled"),      # configs[0]'s 16 KiB pieces (2048 units x 4 tiles); auto = 2^10 / 32
     (32, 6, 8, "xor", "blocks"),      # 5-8 rows: the u64-entry (NW=2) tile
     (24, 2, 3, "xor", "split"),       # 8 groups: mid-tile local stores
     (16, 3, 4, "literal", "blocks"),  # zero L blocks
@@ -367,8 +368,8 @@ def test_write_window_same_bytes(E, torch, orc, schedule, k, m, r, local, layout
     enc_window_*) only delays the
     parity stores: encodes with it forced off, on, and at another period give
     identical parities, equal to the oracle on a column window, and the default
-    choice ('auto': slabs and pointer modes at k >= 64, <= 4 global rows, blocks or tiled pieces
-    >= 8 KiB, >= 8192 tiles) is one of them. With the window on, the <= 4-row tile keeps
+    choice ('auto': slabs and pointer modes at k >= 24 (a 2^10-tick period below k = 64),
+    <= 4 global rows, blocks or tiled pieces >= 8 KiB, >= 8192 tiles) gives them too. With the window on, the <= 4-row tile keeps
     three rows in flight (ECW_TILE_ASM3): k = 3, 4, 5, 9, 10 reach each tail of
     that ring."""
     B, S = 1 << 20, 32  # 32 stripes x 256 tiles = 8192 tiles
