@@ -390,6 +390,73 @@
 #define ECW_LOAD_C "global_load_dwordx4 v[36:39], v40, s[40:41]" ECW_ASM_LDMOD "\n\t"
 #define ECW_ROW_C(XL) ECW_ROW("v36", "v37", "v38", "v39", XL)
 #define ECW_ROW_PRE_C(XL) ECW_ROW_PRE("v36", "v37", "v38", "v39", XL)
+// The three-slot row loop of every asm tile (P = ECW / ECW2 / ECW4: that tile's
+// STEP / ROW / ROW_DRAIN macros; slot C = v[36:39], idle until the global rows):
+// rows j, j+1, j+2 in flight, each consumption behind vmcnt(2); the tail takes the
+// last 3, 4 or 5 rows. Needs k >= 3.
+#define ECW_RING3_ROWS(P, BND, XL, MODE)                                            \
+  /* main loop: rows j..j+2 while rows j+3..j+5 exist */                    \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 5\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_C(XL), ECW_LOAD_C, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  /* 3, 4 or 5 rows left (k - j); slots A, B, C hold rows j, j+1, j+2 */    \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc1 12f\n\t"                                                  \
+  "s_cmp_eq_u32 s49, 4\n\t"                                                 \
+  "s_cbranch_scc1 14f\n\t"                                                  \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_B(XL), ECW_LOAD_B, , BND)                     \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_ROW_C(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  P##_ROW_A(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  P##_ROW_B(XL) BND                                                         \
+  "s_branch 13f\n\t"                                                        \
+  "14:\n\t"                                                                 \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_STEP_##MODE(P##_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                     \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_ROW_B(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  P##_ROW_C(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  P##_ROW_A(XL) BND                                                         \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(2)\n\t"                                                  \
+  P##_ROW_A(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  P##_ROW_B(XL) BND                                                         \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  P##_ROW_C(XL) BND                                                         \
+  "13:\n\t"                                                                 \
+  P##_ROW_DRAIN
+
 #define ECW_TILE_ASM3(BND, XL, END, MODE)                                          \
   "v_mov_b32 v40, %[col]\n\t"                                               \
   "v_mov_b32 v33, 0x3c3c3c3c\n\t"                                           \
@@ -412,67 +479,7 @@
   "s_mov_b32 s46, %[lds]\n\t"                                               \
   ECW_LPTR_INIT_##MODE                                                      \
   "s_min_u32 s45, %[r], %[k]\n\t"                                           \
-  /* main loop: rows j..j+2 while rows j+3..j+5 exist */                    \
-  "10:\n\t"                                                                 \
-  "s_add_u32 s49, s44, 5\n\t"                                               \
-  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
-  "s_cbranch_scc1 11f\n\t"                                                  \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND)   \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_C(XL), ECW_LOAD_C, ECW_NEXTROW_##MODE, BND)   \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_branch 10b\n\t"                                                        \
-  /* 3, 4 or 5 rows left (k - j); slots A, B, C hold rows j, j+1, j+2 */    \
-  "11:\n\t"                                                                 \
-  "s_sub_u32 s49, %[k], s44\n\t"                                            \
-  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
-  "s_cbranch_scc1 12f\n\t"                                                  \
-  "s_cmp_eq_u32 s49, 4\n\t"                                                 \
-  "s_cbranch_scc1 14f\n\t"                                                  \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND)   \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_B(XL), ECW_LOAD_B, , BND)                     \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_ROW_C(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_A(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(0)\n\t"                                                  \
-  ECW_ROW_B(XL) BND                                                         \
-  "s_branch 13f\n\t"                                                        \
-  "14:\n\t"                                                                 \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_STEP_##MODE(ECW_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                     \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_ROW_B(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_C(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(0)\n\t"                                                  \
-  ECW_ROW_A(XL) BND                                                         \
-  "s_branch 13f\n\t"                                                        \
-  "12:\n\t"                                                                 \
-  "s_waitcnt vmcnt(2)\n\t"                                                  \
-  ECW_ROW_A(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW_ROW_B(XL) BND                                                         \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(0)\n\t"                                                  \
-  ECW_ROW_C(XL) BND                                                         \
-  "13:\n\t"                                                                 \
-  ECW_ROW_DRAIN                                                             \
+  ECW_RING3_ROWS(ECW, BND, XL, MODE)                                        \
   ECW_WRITE_WINDOW                                                          \
   END                                                                       \
   ECW_GLOBAL_ROWS(MODE)
@@ -629,7 +636,9 @@
   "v_perm_b32 v35, " C15 ", " C14 ", s58\n\t"                               \
   "v_or_b32 v39, v34, v35\n\t"
 
-#define ECW2_TILE_ASM(BND, XL, END, MODE)                                          \
+// set-up of the 5-8-row tile: constants, the first ring loads (ONE_MORE: a third,
+// into slot C), zeroed accumulators, row / group counters
+#define ECW2_TILE_INIT(MODE, ONE_MORE)                                            \
   "v_mov_b32 v40, %[col]\n\t"                                               \
   "v_mov_b32 v33, 0xf0f0f0f0\n\t"                                           \
   "v_mov_b32 v41, 0xff\n\t"                                                 \
@@ -640,6 +649,7 @@
   ECW_ROWPTR_INIT_##MODE                                                    \
   ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
   ECW_LOAD_B ECW_NEXTROW_##MODE                                             \
+  ONE_MORE                                                                  \
   "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
   "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
   "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
@@ -655,6 +665,42 @@
   "s_mov_b32 s46, %[lds]\n\t"                                               \
   ECW_LPTR_INIT_##MODE                                                      \
   "s_min_u32 s45, %[r], %[k]\n\t"                                           \
+
+// global rows l: byte (l & 3) of bank l >> 2 -> output row l (v[36:39])
+#define ECW2_GLOBAL_ROWS(MODE)                                                    \
+  ECW_GPTR_INIT_##MODE                                                      \
+  "s_mov_b32 s56, 0\n\t"                                                    \
+  "30:\n\t"                                                                 \
+  "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
+  "s_cbranch_scc1 31f\n\t"                                                  \
+  "s_and_b32 s49, s56, 3\n\t"                                               \
+  "s_add_u32 s57, s49, 4\n\t"                                               \
+  "s_lshl_b32 s58, s57, 24\n\t"                                             \
+  "s_lshl_b32 s57, s57, 8\n\t"                                              \
+  "s_or_b32 s57, s57, s49\n\t"                                              \
+  "s_or_b32 s57, s57, 0x0c0c0000\n\t"                                       \
+  "s_lshl_b32 s49, s49, 16\n\t"                                             \
+  "s_or_b32 s58, s58, s49\n\t"                                              \
+  "s_or_b32 s58, s58, 0x0c0c\n\t"                                           \
+  "s_cmp_ge_u32 s56, 4\n\t"                                                 \
+  "s_cbranch_scc1 32f\n\t"                                                  \
+  ECW2_TRANSPOSE("v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19",    \
+                 "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27")    \
+  "s_branch 33f\n\t"                                                        \
+  "32:\n\t"                                                                 \
+  ECW2_TRANSPOSE("v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81",    \
+                 "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89")    \
+  "33:\n\t"                                                                 \
+  ECW_GPTR_GET_##MODE                                                       \
+  ECW_ASM_GSTORE("v[36:39]", "s[54:55]")                                    \
+  "s_nop 1\n\t"                                                             \
+  ECW_GPTR_NEXT_##MODE                                                      \
+  "s_add_u32 s56, s56, 1\n\t"                                               \
+  "s_branch 30b\n\t"                                                        \
+  "31:"
+
+#define ECW2_TILE_ASM(BND, XL, END, MODE)                                          \
+  ECW2_TILE_INIT(MODE, )                                                    \
   "10:\n\t"                                                                 \
   "s_add_u32 s49, s44, 3\n\t"                                               \
   "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
@@ -689,37 +735,17 @@
   ECW2_ROW_DRAIN                                                            \
   ECW_WRITE_WINDOW                                                          \
   END                                                                       \
-  /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \
-  ECW_GPTR_INIT_##MODE                                                      \
-  "s_mov_b32 s56, 0\n\t"                                                    \
-  "30:\n\t"                                                                 \
-  "s_cmp_ge_u32 s56, %[nrows]\n\t"                                          \
-  "s_cbranch_scc1 31f\n\t"                                                  \
-  "s_and_b32 s49, s56, 3\n\t"                                               \
-  "s_add_u32 s57, s49, 4\n\t"                                               \
-  "s_lshl_b32 s58, s57, 24\n\t"                                             \
-  "s_lshl_b32 s57, s57, 8\n\t"                                              \
-  "s_or_b32 s57, s57, s49\n\t"                                              \
-  "s_or_b32 s57, s57, 0x0c0c0000\n\t"                                       \
-  "s_lshl_b32 s49, s49, 16\n\t"                                             \
-  "s_or_b32 s58, s58, s49\n\t"                                              \
-  "s_or_b32 s58, s58, 0x0c0c\n\t"                                           \
-  "s_cmp_ge_u32 s56, 4\n\t"                                                 \
-  "s_cbranch_scc1 32f\n\t"                                                  \
-  ECW2_TRANSPOSE("v12", "v13", "v14", "v15", "v16", "v17", "v18", "v19",    \
-                 "v20", "v21", "v22", "v23", "v24", "v25", "v26", "v27")    \
-  "s_branch 33f\n\t"                                                        \
-  "32:\n\t"                                                                 \
-  ECW2_TRANSPOSE("v74", "v75", "v76", "v77", "v78", "v79", "v80", "v81",    \
-                 "v82", "v83", "v84", "v85", "v86", "v87", "v88", "v89")    \
-  "33:\n\t"                                                                 \
-  ECW_GPTR_GET_##MODE                                                       \
-  ECW_ASM_GSTORE("v[36:39]", "s[54:55]")                                    \
-  "s_nop 1\n\t"                                                             \
-  ECW_GPTR_NEXT_##MODE                                                      \
-  "s_add_u32 s56, s56, 1\n\t"                                               \
-  "s_branch 30b\n\t"                                                        \
-  "31:"
+  ECW2_GLOBAL_ROWS(MODE)
+
+// the three-slot ring of the 5-8-row tile (slot C = v[36:39], as ECW_TILE_ASM3)
+#define ECW2_ROW_C(XL) ECW2_ROW("v36", "v37", "v38", "v39", XL)
+#define ECW2_ROW_PRE_C(XL) ECW2_ROW_PRE("v36", "v37", "v38", "v39", XL)
+#define ECW2_TILE_ASM3(BND, XL, END, MODE)                                         \
+  ECW2_TILE_INIT(MODE, "s_waitcnt lgkmcnt(0)\n\t" ECW_LOAD_C ECW_NEXTROW_##MODE) \
+  ECW_RING3_ROWS(ECW2, BND, XL, MODE)                                       \
+  ECW_WRITE_WINDOW                                                          \
+  END                                                                       \
+  ECW2_GLOBAL_ROWS(MODE)
 
 #define ECW2_TILE_OPERANDS                                                          \
   ECW_TILE_OPERANDS, "s63", "v57", "v58", "v59", "v60", "v61", "v62", "v63", "v64", "v65", "v66", "v67",  \
@@ -907,7 +933,8 @@
   ECW_UNPARK(4, "v[138:141]", MODE)                                         \
   "27:\n\t"
 
-#define ECW4_TILE_ASM(BND, XL, END, MODE)                                          \
+// set-up of the 9-16-row tile (ONE_MORE: a third ring load, into slot C)
+#define ECW4_TILE_INIT(MODE, ONE_MORE)                                            \
   "v_mov_b32 v40, %[col]\n\t"                                               \
   "v_mov_b32 v33, 0xf0f0f0f0\n\t"                                           \
   "s_mov_b32 s50, 0x0c050400\n\t"                                           \
@@ -917,6 +944,7 @@
   ECW_ROWPTR_INIT_##MODE                                                    \
   ECW_LOAD_A ECW_NEXTROW_##MODE "s_waitcnt lgkmcnt(0)\n\t"                  \
   ECW_LOAD_B ECW_NEXTROW_##MODE                                             \
+  ONE_MORE                                                                  \
   "v_mov_b32 v12, 0\n\tv_mov_b32 v13, 0\n\tv_mov_b32 v14, 0\n\tv_mov_b32 v15, 0\n\t" \
   "v_mov_b32 v16, 0\n\tv_mov_b32 v17, 0\n\tv_mov_b32 v18, 0\n\tv_mov_b32 v19, 0\n\t" \
   "v_mov_b32 v20, 0\n\tv_mov_b32 v21, 0\n\tv_mov_b32 v22, 0\n\tv_mov_b32 v23, 0\n\t" \
@@ -940,41 +968,9 @@
   "s_mov_b32 s46, %[lds]\n\t"                                               \
   ECW_LPTR_INIT_##MODE                                                      \
   "s_min_u32 s45, %[r], %[k]\n\t"                                           \
-  "10:\n\t"                                                                 \
-  "s_add_u32 s49, s44, 3\n\t"                                               \
-  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
-  "s_cbranch_scc1 11f\n\t"                                                  \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND) \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW4_STEP_##MODE(ECW4_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND) \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_branch 10b\n\t"                                                        \
-  "11:\n\t"                                                                 \
-  "s_sub_u32 s49, %[k], s44\n\t"                                            \
-  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
-  "s_cbranch_scc0 12f\n\t"                                                  \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                   \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW4_ROW_B(XL) BND                                                        \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(0)\n\t"                                                  \
-  ECW4_ROW_A(XL) BND                                                        \
-  "s_branch 13f\n\t"                                                        \
-  "12:\n\t"                                                                 \
-  "s_waitcnt vmcnt(1)\n\t"                                                  \
-  ECW4_ROW_A(XL) BND                                                        \
-  "s_add_u32 s44, s44, 1\n\t"                                               \
-  "s_waitcnt vmcnt(0)\n\t"                                                  \
-  ECW4_ROW_B(XL) BND                                                        \
-  "13:\n\t"                                                                 \
-  ECW4_ROW_DRAIN                                                            \
-  ECW_WRITE_WINDOW                                                          \
-  END                                                                       \
-  /* global rows l: byte (l & 3) of bank l >> 2 -> output row l */          \
+
+// global rows l: byte (l & 3) of bank l >> 2 -> output row l (v[36:39])
+#define ECW4_GLOBAL_ROWS(MODE)                                                    \
   ECW_GPTR_INIT_##MODE                                                      \
   "s_mov_b32 s56, 0\n\t"                                                    \
   "30:\n\t"                                                                 \
@@ -1018,6 +1014,53 @@
   "s_branch 30b\n\t"                                                        \
   "31:"
 
+#define ECW4_TILE_ASM(BND, XL, END, MODE)                                          \
+  ECW4_TILE_INIT(MODE, )                                                    \
+  "10:\n\t"                                                                 \
+  "s_add_u32 s49, s44, 3\n\t"                                               \
+  "s_cmp_ge_u32 s49, %[k]\n\t"                                              \
+  "s_cbranch_scc1 11f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, ECW_NEXTROW_##MODE, BND) \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_B(XL), ECW_LOAD_B, ECW_NEXTROW_##MODE, BND) \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_branch 10b\n\t"                                                        \
+  "11:\n\t"                                                                 \
+  "s_sub_u32 s49, %[k], s44\n\t"                                            \
+  "s_cmp_eq_u32 s49, 3\n\t"                                                 \
+  "s_cbranch_scc0 12f\n\t"                                                  \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_STEP_##MODE(ECW4_ROW_PRE_A(XL), ECW_LOAD_A, , BND)                   \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_ROW_B(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW4_ROW_A(XL) BND                                                        \
+  "s_branch 13f\n\t"                                                        \
+  "12:\n\t"                                                                 \
+  "s_waitcnt vmcnt(1)\n\t"                                                  \
+  ECW4_ROW_A(XL) BND                                                        \
+  "s_add_u32 s44, s44, 1\n\t"                                               \
+  "s_waitcnt vmcnt(0)\n\t"                                                  \
+  ECW4_ROW_B(XL) BND                                                        \
+  "13:\n\t"                                                                 \
+  ECW4_ROW_DRAIN                                                            \
+  ECW_WRITE_WINDOW                                                          \
+  END                                                                       \
+  ECW4_GLOBAL_ROWS(MODE)
+
+#define ECW4_ROW_C(XL) ECW4_ROW("v36", "v37", "v38", "v39", XL)
+#define ECW4_ROW_PRE_C(XL) ECW4_ROW_PRE("v36", "v37", "v38", "v39", XL)
+#define ECW4_TILE_ASM3(BND, XL, END, MODE)                                         \
+  ECW4_TILE_INIT(MODE, "s_waitcnt lgkmcnt(0)\n\t" ECW_LOAD_C ECW_NEXTROW_##MODE) \
+  ECW_RING3_ROWS(ECW4, BND, XL, MODE)                                       \
+  ECW_WRITE_WINDOW                                                          \
+  END                                                                       \
+  ECW4_GLOBAL_ROWS(MODE)
+
 #define ECW4_TILE_OPERANDS                                                          \
   ECW2_TILE_OPERANDS, "v90", "v91", "v92", "v93", "v94", "v95", "v96", "v97", "v98", "v99",        \
     "v100", "v101", "v102", "v103", "v104", "v105", "v106", "v107", "v108", "v109", "v110", "v111", \
@@ -1047,29 +1090,29 @@ namespace {
                      ECW_TILE_OPERANDS);                                                 \
   }
 
-#define ECW2_TILE_CALL(MODE)                                                             \
+#define ECW2_TILE_CALL(TILE, MODE)                                                           \
   if constexpr (LOCAL == kLocalNone) {                                                   \
-    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW2_TILE_OPERANDS);         \
+    asm volatile(TILE(ECW_BOUNDARY_NONE, 0, , MODE) ECW2_TILE_OPERANDS);         \
   } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
-    asm volatile(ECW2_TILE_ASM(ECW2_BOUNDARY_PARK, 1, ECW2_STORE_PARKED(MODE), MODE)     \
+    asm volatile(TILE(ECW2_BOUNDARY_PARK, 1, ECW2_STORE_PARKED(MODE), MODE)     \
                      ECW2_TILE_OPERANDS_PARK);                                           \
   } else if constexpr (LOCAL == kLocalXor) {                                             \
-    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW2_TILE_OPERANDS);     \
+    asm volatile(TILE(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW2_TILE_OPERANDS);     \
   } else {                                                                               \
-    asm volatile(ECW2_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
+    asm volatile(TILE(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
                      ECW2_TILE_OPERANDS);                                                \
   }
 
-#define ECW4_TILE_CALL(MODE)                                                             \
+#define ECW4_TILE_CALL(TILE, MODE)                                                           \
   if constexpr (LOCAL == kLocalNone) {                                                   \
-    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY_NONE, 0, , MODE) ECW4_TILE_OPERANDS);         \
+    asm volatile(TILE(ECW_BOUNDARY_NONE, 0, , MODE) ECW4_TILE_OPERANDS);         \
   } else if constexpr (LOCAL == kLocalXor && PARK) {                                     \
-    asm volatile(ECW4_TILE_ASM(ECW4_BOUNDARY_PARK, 1, ECW4_STORE_PARKED(MODE), MODE)     \
+    asm volatile(TILE(ECW4_BOUNDARY_PARK, 1, ECW4_STORE_PARKED(MODE), MODE)     \
                      ECW4_TILE_OPERANDS_PARK);                                           \
   } else if constexpr (LOCAL == kLocalXor) {                                             \
-    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW4_TILE_OPERANDS);     \
+    asm volatile(TILE(ECW_BOUNDARY(1, MODE), 1, , MODE) ECW4_TILE_OPERANDS);     \
   } else {                                                                               \
-    asm volatile(ECW4_TILE_ASM(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
+    asm volatile(TILE(ECW_BOUNDARY_COUNT, 0, ECW_STORE_ZEROS(MODE), MODE)         \
                      ECW4_TILE_OPERANDS);                                                \
   }
 
@@ -1082,17 +1125,35 @@ __device__ __forceinline__ void encode_tile_asm(const uint8_t* row0, uint8_t* lr
   const uint32_t bslo = static_cast<uint32_t>(bstride), bshi = static_cast<uint32_t>(bstride >> 32);
   const uint32_t pbslo = static_cast<uint32_t>(pbstride), pbshi = static_cast<uint32_t>(pbstride >> 32);
   const bool ring3 = k >= 3 && (kAsmRing3 == 2 || (kAsmRing3 == 1 && ww != 0));  // uniform: a scalar branch
+  const bool ring3_nw2 = k >= 3 && kAsmRing3Nw2 != 0;
+  const bool ring3_nw4 = k >= 3 && kAsmRing3Nw4 != 0;
   if constexpr (NW == 4) {
     if constexpr (TAB) {
-      ECW4_TILE_CALL(TAB)
+      if (ring3_nw4) {
+        ECW4_TILE_CALL(ECW4_TILE_ASM3, TAB)
+      } else {
+        ECW4_TILE_CALL(ECW4_TILE_ASM, TAB)
+      }
     } else {
-      ECW4_TILE_CALL(SLAB)
+      if (ring3_nw4) {
+        ECW4_TILE_CALL(ECW4_TILE_ASM3, SLAB)
+      } else {
+        ECW4_TILE_CALL(ECW4_TILE_ASM, SLAB)
+      }
     }
   } else if constexpr (NW == 2) {
     if constexpr (TAB) {
-      ECW2_TILE_CALL(TAB)
+      if (ring3_nw2) {
+        ECW2_TILE_CALL(ECW2_TILE_ASM3, TAB)
+      } else {
+        ECW2_TILE_CALL(ECW2_TILE_ASM, TAB)
+      }
     } else {
-      ECW2_TILE_CALL(SLAB)
+      if (ring3_nw2) {
+        ECW2_TILE_CALL(ECW2_TILE_ASM3, SLAB)
+      } else {
+        ECW2_TILE_CALL(ECW2_TILE_ASM, SLAB)
+      }
     }
   } else if constexpr (TAB) {
     if (ring3) {

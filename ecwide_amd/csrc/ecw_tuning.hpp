@@ -47,6 +47,17 @@
 // -0.5..+0.5 % at k = 128, -1.2..-2.1 % at k = 32; profiles/r05h_*, r05i_*)
 #define ECW_ASM_RING3 1
 #endif
+#ifndef ECW_ASM_RING3_NW2
+// 5-8-row asm tile: three rows in flight per wave (slot C in v[36:39], same 110 /
+// 90 VGPRs): +1.2..2.3 % over block slabs at k = 32 / 128, +3.6 % over pointer
+// tables (profiles/r05u_nw2_ring3_*); 0 = the two-slot ring
+#define ECW_ASM_RING3_NW2 1
+#endif
+#ifndef ECW_ASM_RING3_NW4
+// 9-16-row asm tile: three rows in flight per wave (slot C in v[36:39], same 142 /
+// 123 VGPRs): +0.3..1.2 % at k = 64 / 128, +4.4 % at k = 32 (profiles/r05v_ring3_*)
+#define ECW_ASM_RING3_NW4 1
+#endif
 #ifndef ECW_ASM_TPB1
 #define ECW_ASM_TPB1 1  // <= 4 rows (2: tiled +-0, block slab -1.2 %, profiles/r03_tpb1_ab.log)
 #endif
@@ -93,6 +104,8 @@ constexpr int kPrefetchEnc = ECW_PREFETCH_ENC;
 constexpr int kPrefetchEncAsmTail = 2;  // the asm launches' ragged-tail kernel
 constexpr int kAsmRing3 = ECW_ASM_RING3;
 static_assert(kAsmRing3 >= 0 && kAsmRing3 <= 2, "ECW_ASM_RING3: 0, 1 or 2");
+constexpr int kAsmRing3Nw2 = ECW_ASM_RING3_NW2;
+constexpr int kAsmRing3Nw4 = ECW_ASM_RING3_NW4;
 constexpr uint64_t kGridPerCu = ECW_GRID_PER_CU;
 constexpr uint64_t kGridPerCuXor = ECW_GRID_PER_CU_XOR;
 constexpr int kPrefetchXor = ECW_PREFETCH_XOR;
