@@ -2,7 +2,8 @@
 # Round 5, check of the tree with the paired K = 4 repair default: smoke, the
 # GPU suite, the placement study (auto = paired K = 4 + window) in one process,
 # the default bench under the kernel tracer and plain, FETCH / WRITE passes of
-# the bench's repair, and configs[3] (--hbm-fill) under the tracer.
+# the bench's repair, and configs[3] (--hbm-fill) under the tracer; with
+# TWO_RANK=1 also bench.py --gpus 2 with both ranks on the one GPU.
 # Run: gpurun -- 'bash tools/gpu_r05_g.sh'
 set -uo pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
@@ -27,3 +28,7 @@ tail -1 $O/hbmfill_traced.log | cut -c1-200
 cd $R
 timeout -k 10 600 python bench.py > $O/bench_default.log 2>&1 || exit $?
 tail -1 $O/bench_default.log | cut -c1-300
+if [ -n "${TWO_RANK:-}" ]; then
+  timeout -k 10 600 python bench.py --gpus 2 --steps 10 --configs4-steps 2 --shape-steps 2 --other-layout-steps 0 > $O/bench_2rank.log 2>&1 || exit $?
+  tail -1 $O/bench_2rank.log | cut -c1-300
+fi
