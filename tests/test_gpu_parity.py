@@ -892,6 +892,8 @@ def test_random_sweep_vs_oracle(E, torch, orc):
     ("C", 200, 10, 40, 4096 + 1, 1),       # wide k: 100 KiB of tables (> 64 KiB of dynamic LDS)
     ("C", 128, 9, 27, 8192, 3),            # 9 rows + 5 parked XOR locals
     ("R", 128, 20, 0, 4096, 1),            # 20 rows: a 16-row pass and a 4-row pass
+    ("R", 21, 10, 0, 4096 + 16, 2),        # k = 21: the three-slot ring's 3-row tail, every addressing mode
+    ("C", 21, 6, 5, 4096, 2),              # the same tail in the 5-8-row tile (5 groups, parked)
 ])
 def test_more_than_8_global_rows(E, torch, orc, code, k, m, r, B, S):
     """ECWide-C's RS / TL / CL codecs take any m (NativeCodec.java:20-54):
