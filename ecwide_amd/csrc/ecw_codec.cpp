@@ -31,6 +31,7 @@
 #include "../../include/ecwide.h"
 #include "ecw_gf.hpp"
 #include "ecw_internal.hpp"
+#include "ecw_tuning.hpp"
 
 using namespace ecw;
 
@@ -1179,31 +1180,59 @@ constexpr size_t kHostChunk = size_t(8) << 20;
 constexpr size_t kSmallBlock = size_t(256) << 10;  // blocks up to this size take the packed path
 constexpr int kSlots = 3;
 
+// Host -> HBM copies of a slice go out on kHostInStreams streams (block b on
+// stream b % kHostInStreams): one copy queue moves 8 MiB copies at ~53.5 GB/s,
+// two together at ~57 GB/s, PCIe Gen5 x16's practical rate
+// (profiles/r05h2d_probe.log).
 struct HostPipe {
-  hipStream_t s_in = nullptr, s_run = nullptr, s_out = nullptr;
-  hipEvent_t ev_in[kSlots] = {}, ev_run[kSlots] = {}, ev_out[kSlots] = {};
+  hipStream_t s_in[kHostInStreams] = {}, s_run = nullptr, s_out = nullptr;
+  hipEvent_t ev_in[kHostInStreams][kSlots] = {}, ev_run[kSlots] = {}, ev_out[kSlots] = {};
   bool ok = false;
   int init() {
     if (ok) return ECW_OK;
-    for (hipStream_t* st : {&s_in, &s_run, &s_out})
+    for (hipStream_t& st : s_in)
+      if (hipStreamCreateWithFlags(&st, hipStreamNonBlocking) != hipSuccess) return ECW_EDEVICE;
+    for (hipStream_t* st : {&s_run, &s_out})
       if (hipStreamCreateWithFlags(st, hipStreamNonBlocking) != hipSuccess) return ECW_EDEVICE;
-    for (int i = 0; i < kSlots; ++i)
-      for (hipEvent_t* e : {&ev_in[i], &ev_run[i], &ev_out[i]})
+    for (int i = 0; i < kSlots; ++i) {
+      for (auto& q : ev_in)
+        if (hipEventCreateWithFlags(&q[i], hipEventDisableTiming) != hipSuccess) return ECW_EDEVICE;
+      for (hipEvent_t* e : {&ev_run[i], &ev_out[i]})
         if (hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess) return ECW_EDEVICE;
+    }
     ok = true;
     return ECW_OK;
   }
   void destroy(int device) {
-    for (hipStream_t st : {s_in, s_run, s_out}) grave::release(st, grave::kStream, device);
-    for (int i = 0; i < kSlots; ++i)
-      for (hipEvent_t e : {ev_in[i], ev_run[i], ev_out[i]}) grave::release(e, grave::kEvent, device);
+    for (hipStream_t st : s_in) grave::release(st, grave::kStream, device);
+    for (hipStream_t st : {s_run, s_out}) grave::release(st, grave::kStream, device);
+    for (int i = 0; i < kSlots; ++i) {
+      for (auto& q : ev_in) grave::release(q[i], grave::kEvent, device);
+      for (hipEvent_t e : {ev_run[i], ev_out[i]}) grave::release(e, grave::kEvent, device);
+    }
+  }
+  hipStream_t in(size_t b) const { return s_in[b % kHostInStreams]; }
+  // slot `slot` may be refilled once its previous D2H copies are done
+  bool wait_slot_free(int slot) const {
+    for (hipStream_t st : s_in)
+      if (hipStreamWaitEvent(st, ev_out[slot], 0) != hipSuccess) return false;
+    return true;
+  }
+  // the kernel on slot `slot` waits for every input stream's copies into it
+  bool inputs_ready(int slot) {
+    for (int q = 0; q < kHostInStreams; ++q)
+      if (hipEventRecord(ev_in[q][slot], s_in[q]) != hipSuccess || hipStreamWaitEvent(s_run, ev_in[q][slot], 0) != hipSuccess)
+        return false;
+    return true;
   }
 };
 
 // error exit of a pipelined call: let the copies already queued on the
 // pipeline's streams finish before the caller may free its buffers
 static int drain(HostPipe& P, int st) {
-  for (hipStream_t x : {P.s_in, P.s_run, P.s_out})
+  for (hipStream_t x : P.s_in)
+    if (x) (void)hipStreamSynchronize(x);
+  for (hipStream_t x : {P.s_run, P.s_out})
     if (x) (void)hipStreamSynchronize(x);
   return st;
 }
@@ -1256,11 +1285,10 @@ static int host_roundtrip(ecw_codec* c, const uint8_t* const* in, int nin, uint8
     uint8_t* base = c->d_stage + slot * slot_bytes;
     for (int b = 0; b < nin; ++b) din[b] = base + b * cstride;
     for (int b = 0; b < nout; ++b) dout[b] = base + (nin + b) * cstride;
-    if (i >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (i >= kSlots && !P.wait_slot_free(slot)) return drain(P, ECW_EDEVICE);
     for (int b = 0; b < nin; ++b)
-      if (hipMemcpyAsync(din[b], in[b] + c0, n, hipMemcpyHostToDevice, P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
-    if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
-    if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
+      if (hipMemcpyAsync(din[b], in[b] + c0, n, hipMemcpyHostToDevice, P.in(b)) != hipSuccess) return drain(P, ECW_EDEVICE);
+    if (!P.inputs_ready(slot)) return drain(P, ECW_EDEVICE);
     if ((st = op(c, din.data(), nin, dout.data(), nout, n, P.s_run))) return drain(P, st);
     if (hipEventRecord(P.ev_run[slot], P.s_run) != hipSuccess) return drain(P, ECW_EDEVICE);
     if (hipStreamWaitEvent(P.s_out, P.ev_run[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
@@ -1888,14 +1916,13 @@ int ecw_encode_stripes(ecw_codec* c, int stripes, const uint8_t* const* data, ui
       const int slot = static_cast<int>(step % kSlots);
       const size_t n = std::min(chunk, len - c0);
       uint8_t* base = c->d_stage + slot * slot_bytes;
-      if (step >= kSlots && hipStreamWaitEvent(P.s_in, P.ev_out[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
+      if (step >= kSlots && !P.wait_slot_free(slot)) return drain(P, ECW_EDEVICE);
       for (int s = 0; s < ns; ++s)
         for (int j = 0; j < k; ++j)
           if (hipMemcpyAsync(base + s * stripe_bytes + j * cstride, data[static_cast<size_t>(s0 + s) * k + j] + c0, n,
-                             hipMemcpyHostToDevice, P.s_in) != hipSuccess)
+                             hipMemcpyHostToDevice, P.in(static_cast<size_t>(s) * k + j)) != hipSuccess)
             return drain(P, ECW_EDEVICE);
-      if (hipEventRecord(P.ev_in[slot], P.s_in) != hipSuccess) return drain(P, ECW_EDEVICE);
-      if (hipStreamWaitEvent(P.s_run, P.ev_in[slot], 0) != hipSuccess) return drain(P, ECW_EDEVICE);
+      if (!P.inputs_ready(slot)) return drain(P, ECW_EDEVICE);
       const SlabRows slab = slab_rows(base, cstride, stripe_bytes, k);
       EncodeTarget t;
       t.slab = &slab;

@@ -94,6 +94,11 @@
 #define ECW_XOR_SKEW_K 4  // diagonal skew of whole blocks; must be one of kXorSkews
 #endif
 
+// ---- host-memory pipeline -------------------------------------------------------
+#ifndef ECW_HOST_IN_STREAMS
+#define ECW_HOST_IN_STREAMS 2  // host -> HBM copy streams of the pipelined host calls (1 or 2)
+#endif
+
 // ---- request service -------------------------------------------------------------
 #ifndef ECW_SVC_COLD_SLEEPS
 #define ECW_SVC_COLD_SLEEPS 2  // s_sleep 127 (~3.4 us each) after every poll of a cold slot
@@ -116,4 +121,6 @@ constexpr int kMaxParkedLocals = 5;  // v[58:77] of the asm tile: <= 5 local par
 constexpr int64_t kCohortTiles = ECW_COHORT_TILES;
 constexpr unsigned long long kTicketMinTiles = ECW_TICKET_MIN_TILES;
 constexpr int kSvcColdSleeps = ECW_SVC_COLD_SLEEPS;
+constexpr int kHostInStreams = ECW_HOST_IN_STREAMS;
+static_assert(kHostInStreams == 1 || kHostInStreams == 2, "ECW_HOST_IN_STREAMS: 1 or 2");
 }  // namespace ecw
