@@ -88,7 +88,7 @@
 #define ECW_GRID_PER_CU_XOR 2048  // one workgroup per tile up to 512 Ki tiles (+8.6 % at the HBM-filling batch vs 512)
 #endif
 #ifndef ECW_XOR_WINDOW
-#define ECW_XOR_WINDOW 8  // straight-line kernel: loads in flight per wave (4..27 within +-0.5 %)
+#define ECW_XOR_WINDOW 8  // straight-line kernel: loads in flight per wave (4..27 within +-0.5 % in round 4; round 5 at r = 8 / 11 / 27: 4 -0.1..-1.1 %, 16 -0.9..-3.9 %, profiles/r05xw_*)
 #endif
 #ifndef ECW_XOR_SKEW_K
 #define ECW_XOR_SKEW_K 4  // diagonal skew of whole blocks; must be one of kXorSkews
