@@ -59,7 +59,7 @@
 #define ECW_ASM_RING3_NW4 1
 #endif
 #ifndef ECW_ASM_TPB1
-#define ECW_ASM_TPB1 1  // <= 4 rows (2: tiled +-0, block slab -1.2 %, profiles/r03_tpb1_ab.log; under the window tiled -0.5..-1.6 %, r05tp_*)
+#define ECW_ASM_TPB1 1  // <= 4 rows (2: tiled +-0, block slab -1.2 %, profiles/r03_tpb1_ab.log; under the window tiled -0.5..-1.6 %, r05tp_*; pointer tables / block slab -0.6..-1.5 %, r05pt_*)
 #endif
 // The slab is encoded in launch windows of one grid's worth of tiles (256 CUs x
 // ECW_GRID_PER_CU), one tile per workgroup (+3.5 % encode at the 272 GiB slab,
