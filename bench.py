@@ -42,6 +42,8 @@ import subprocess
 import sys
 import time
 
+T_START = time.time()  # the process's start: the time budget and the hard deadline count from here
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
@@ -96,6 +98,20 @@ def parse(argv=None):
                     help="no GPU: plan every rank's share and run the rank orchestration and timing reduction "
                          "only (CPU test of the N>1 path; --dry-run-free-gib stands in for free HBM)")
     ap.add_argument("--dry-run-free-gib", type=float, default=287.0)
+    ap.add_argument("--inject-fail", "--dry-run-fail", dest="inject_fail", default=None,
+                    help="rank=R,leg=NAME[,at=I][,mode=raise|hang|exit]: make rank R fail in leg NAME (at its start, "
+                         "or just before the leg's I-th collective) -- the test of the fail-safe N>1 path")
+    ap.add_argument("--budget-s", type=float, default=450.0,
+                    help="time budget: an optional leg starts only if the elapsed time (max over ranks, from "
+                         "process start) plus its estimate fits (leg_estimates)")
+    ap.add_argument("--deadline-s", type=float, default=540.0,
+                    help="hard deadline after process start: rank 0 prints the line with what it has, every rank "
+                         "exits (a rank stuck in a GPU call included)")
+    ap.add_argument("--collective-timeout", type=float, default=120.0,
+                    help="seconds a leg collective waits for the other ranks before the group counts as broken")
+    ap.add_argument("--profile-csv", default=os.path.join(REPO, "profiles", "r06fin_bench_kernel_stats.csv"),
+                    help="committed rocprofv3 --stats kernel summary of this workload on this kernel build: the "
+                         "line's roofline.profile_frac / profile_repair_frac are recomputed from it")
     ap.add_argument("--pageable", action="store_true",
                     help="with --host-resident: ordinary pageable host blocks instead of pinned ones")
     ap.add_argument("--host-resident", action="store_true",
@@ -126,9 +142,46 @@ def spawn_ranks(n: int, argv: list) -> int:
     return subprocess.run(cmd, env=env).returncode
 
 
+class LegAborted(Exception):
+    """Another rank failed in the current leg: every rank leaves it at the same
+    collective (the one the failing rank's fail-sync matched)."""
+
+
+class GroupBroken(Exception):
+    """A collective timed out or lost a peer (a rank hung or died): no further
+    collective can run in this process."""
+
+
+class InjectedFailure(RuntimeError):
+    """--inject-fail: a deliberate failure on one rank (CPU tests of the N>1
+    path and the one-GPU rehearsal)."""
+
+
+def parse_inject(spec: str | None) -> dict | None:
+    """`rank=R,leg=NAME[,at=I][,mode=raise|hang|exit]`: rank R fails in leg NAME
+    at its start (at=0) or just before the leg's I-th collective."""
+    if not spec:
+        return None
+    kv = dict(x.split("=", 1) for x in spec.split(",") if x)
+    leg = {"host": "host_resident", "chunkgen": "chunk_generator", "cpu": "cpu_baseline"}.get(kv["leg"], kv["leg"])
+    mode = kv.get("mode", "raise")
+    if mode not in ("raise", "hang", "exit") or leg not in LEG_NAMES:
+        raise SystemExit(f"bench.py: bad --inject-fail {spec!r} (legs: {', '.join(LEG_NAMES)})")
+    return {"rank": int(kv["rank"]), "leg": leg, "at": int(kv.get("at", 0)), "mode": mode}
+
+
 class Dist:
-    """World/rank/device of this process and the few collectives the bench
-    uses (barrier, max, gather of one float per rank)."""
+    """World/rank/device of this process and the bench's one collective.
+
+    Every barrier, max, min and gather is `_sync`: ONE all-reduce (sum) of a
+    fixed-shape vector [failures, x of rank 0 .. N-1] on a gloo group with a
+    short timeout. Because every collective has the same shape, a rank that
+    fails inside a leg makes a single fail-sync that stands in for whichever
+    collective the other ranks wait in; they see failures > 0 there and leave
+    the leg together (LegAborted), so an exception on one rank never strands
+    the others in a barrier. A rank that hangs or dies turns into a timeout /
+    closed connection on the others (GroupBroken): they skip every later leg
+    and rank 0 still prints the line (run_leg, Line)."""
 
     def __init__(self, args):
         from ecwide_amd.shard import dist_env
@@ -137,7 +190,11 @@ class Dist:
         if self.world != args.gpus:
             raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={self.world}")
         self.dry = args.dry_run
-        self.dev, self.ndev, self.backend = None, 0, None
+        self.inject = parse_inject(args.inject_fail)
+        self.budget = args.budget_s
+        self.leg, self.leg_sync, self.broken = None, 0, None
+        self.leg_seconds = {}
+        self.dev, self.ndev, self.backend, self.pg = None, 0, None, None
         if not self.dry:
             import torch
 
@@ -150,14 +207,19 @@ class Dist:
             torch.cuda.set_device(self.dev)
         self.distinct = self.dry or self.ndev >= self.world  # refined below from the ranks' PCI ids
         if self.world > 1:
+            import datetime
+
             import torch
             import torch.distributed as dist
 
             # no stripe byte moves between ranks: the only collectives are the
-            # barriers around the timed region and a few scalars (max time, min
+            # barriers around the timed regions and a few scalars (max time, min
             # block size, verification), so they run on gloo over loopback --
-            # the same on one GPU or eight, and no RCCL communicator is set up
-            dist.init_process_group("gloo")
+            # the same on one GPU or eight, and no RCCL communicator is set up.
+            # The rendezvous may wait for a slow first `import torch` on a fresh
+            # box; the legs' collectives get a group with a short timeout.
+            dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(600.0, args.collective_timeout)))
+            self.pg = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=args.collective_timeout))
             self.backend = dist.get_backend()
             if not self.dry:
                 # one process per GPU: which physical GPU each rank drives (PCI
@@ -175,43 +237,226 @@ class Dist:
                     print(f"bench.py: rehearsal: {self.world} ranks share GPUs ({self.ndev} visible per rank)",
                           file=sys.stderr)
 
-    def _tensor(self, vals):
-        import torch
+    # -- the one collective ----------------------------------------------------
+    def _inject_here(self):
+        """--inject-fail: act if this rank, leg and collective index match."""
+        j = self.inject
+        if not j or j["rank"] != self.rank or j["leg"] != self.leg or j["at"] != self.leg_sync:
+            return
+        self.inject = None  # once
+        where = f"rank {self.rank}, leg {self.leg}, before collective {self.leg_sync}"
+        if j["mode"] == "exit":
+            print(f"bench.py: injected exit ({where})", file=sys.stderr, flush=True)
+            os._exit(3)
+        if j["mode"] == "hang":
+            print(f"bench.py: injected hang ({where})", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(3600)
+        raise InjectedFailure(f"injected failure ({where})")
 
-        return torch.tensor(vals, dtype=torch.float64)
-
-    def barrier(self):
-        if self.world > 1:
-            import torch.distributed as dist
-
-            dist.barrier()
-
-    def reduce(self, x: float, op: str) -> float:
-        if self.world == 1:
-            return x
-        import torch.distributed as dist
-
-        t = self._tensor([x])
-        dist.all_reduce(t, op={"max": dist.ReduceOp.MAX, "min": dist.ReduceOp.MIN}[op])
-        return float(t.item())
-
-    def gather(self, x: float) -> list:
-        """x of every rank, in rank order (an all-reduce of a one-hot vector)."""
+    def _sync(self, x: float = 0.0, fail: bool = False) -> list:
+        """All-reduce (sum) of [failures, x on this rank's slot]; returns x of
+        every rank in rank order. Raises LegAborted when another rank reported
+        a failure, GroupBroken when the collective itself failed."""
+        if self.leg is not None:
+            if not fail:
+                self.leg_sync += 1
+                self._inject_here()
         if self.world == 1:
             return [x]
+        if self.broken:
+            raise GroupBroken(self.broken)
+        import torch
         import torch.distributed as dist
 
-        v = [0.0] * self.world
-        v[self.rank] = x
-        t = self._tensor(v)
-        dist.all_reduce(t)
-        return [float(a) for a in t.tolist()]
+        t = torch.zeros(1 + self.world, dtype=torch.float64)
+        t[0] = 1.0 if fail else 0.0
+        t[1 + self.rank] = x
+        try:
+            dist.all_reduce(t, group=self.pg)
+        except Exception as e:  # timeout (a rank hung) or closed connection (a rank died)
+            self.broken = f"collective failed in leg {self.leg}: {type(e).__name__}: {str(e)[:240]}"
+            raise GroupBroken(self.broken) from None
+        if t[0] > 0 and not fail:
+            raise LegAborted(int(t[0].item()))
+        return [float(a) for a in t[1:].tolist()]
+
+    def barrier(self):
+        self._sync()
+
+    def reduce(self, x: float, op: str) -> float:
+        v = self._sync(x)
+        return {"max": max, "min": min}[op](v)
+
+    def gather(self, x: float) -> list:
+        """x of every rank, in rank order."""
+        return self._sync(x)
+
+    def _gather_objects(self, obj) -> list:
+        if self.world == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out = [None] * self.world
+        try:
+            dist.all_gather_object(out, obj, group=self.pg)
+        except Exception as e:
+            self.broken = f"collective failed after leg {self.leg}: {type(e).__name__}: {str(e)[:240]}"
+            raise GroupBroken(self.broken) from None
+        return out
+
+    # -- legs ------------------------------------------------------------------
+    def elapsed_max(self) -> float:
+        """Seconds since the slowest rank's process started (one sync)."""
+        return self.reduce(time.time() - T_START, "max")
+
+    def run_leg(self, name: str, fn, est_s: float = 0.0, local: bool = False):
+        """Run leg `fn` (same collectives on every rank) and return (result,
+        None), or (None, {"error" | "skipped": ...}) on EVERY rank when any
+        rank failed, the group broke or the time budget rules the leg out --
+        never raises. The leg ends with one agreement sync, so a rank's
+        fail-sync is always matched inside the leg it failed in. local: a leg
+        of this rank alone (no collectives: budget on the local clock)."""
+        t0 = time.time()
+        err = None
+        try:
+            if self.broken and not local:
+                return None, {"skipped": f"no collectives after an earlier failure ({self.broken})"}
+            if est_s > 0:
+                # the same elapsed time on every rank (max over ranks), so every rank decides alike
+                el = (time.time() - T_START) if local else self.elapsed_max()
+                if el + est_s > self.budget:
+                    return None, {"skipped": f"time budget: {el:.0f} s elapsed + ~{est_s:.0f} s estimated "
+                                              f"> --budget-s {self.budget:.0f}"}
+            self.leg, self.leg_sync = name, 0
+            self._inject_here()
+            res = fn()
+            if not local:
+                self._sync()  # leg-end agreement: every rank finished the leg
+            return res, None
+        except LegAborted:
+            pass  # this rank was fine; another one failed (its message follows)
+        except GroupBroken as e:
+            return None, {"error": str(e), "rank": self.rank, "collectives": "broken: later legs skipped"}
+        except (Exception, SystemExit) as e:
+            import traceback
+
+            err = f"{type(e).__name__}: {e}"[:600]
+            print(f"bench.py: rank {self.rank} leg {name} failed:\n{traceback.format_exc()}", file=sys.stderr,
+                  flush=True)
+            if self.world == 1 or local:
+                return None, {"error": err, "rank": self.rank}
+            try:
+                self._sync(fail=True)  # stands in for the collective the other ranks wait in
+            except GroupBroken as g:
+                return None, {"error": err, "rank": self.rank, "collectives": f"broken: {g}"}
+        finally:
+            self.leg = None
+            self.leg_seconds[name] = round(time.time() - t0, 2)
+            self._free_device()
+        # aborted on every rank at the same collective: who failed and why
+        try:
+            errs = self._gather_objects(err)
+        except GroupBroken as g:
+            return None, {"error": err or "aborted by another rank", "rank": self.rank,
+                          "collectives": f"broken: {g}"}
+        failed = [i for i, e in enumerate(errs) if e]
+        first = failed[0] if failed else None
+        return None, {"error": errs[first] if failed else "aborted", "rank": first, "failed_ranks": failed}
+
+    def _free_device(self):
+        if not self.dry:
+            import gc
+
+            import torch
+
+            gc.collect()
+            torch.cuda.empty_cache()
 
     def close(self):
         if self.world > 1:
             import torch.distributed as dist
 
-            dist.destroy_process_group()
+            try:
+                dist.destroy_process_group()
+            except Exception:
+                pass
+
+
+class Line:
+    """Rank 0's one JSON line. The legs fill it in as they finish; it is
+    printed exactly once: at the end, or -- with whatever is in it and an
+    `error` -- when the hard deadline (--deadline-s after the process started)
+    passes or the launcher sends SIGTERM (torch.distributed.run does when
+    another rank exits non-zero). A watchdog thread does the last two, so a
+    rank stuck inside a GPU call still gets its line out; every other rank
+    just exits at its deadline."""
+
+    def __init__(self, d: Dist, deadline_s: float):
+        import signal
+        import threading
+
+        self.rank, self.data, self.printed = d.rank, {}, False
+        self.lock = threading.Lock()
+        self.d = d
+        self.deadline = T_START + deadline_s + (0.0 if d.rank == 0 else 5.0)  # rank 0 prints first
+        r, w = os.pipe()
+        os.set_blocking(w, False)
+        signal.signal(signal.SIGTERM, lambda *_: None)  # the watchdog acts on it (set_wakeup_fd)
+        signal.set_wakeup_fd(w)
+        self._r = r
+        threading.Thread(target=self._watch, daemon=True, name="bench-watchdog").start()
+
+    def _watch(self):
+        import select
+
+        while True:
+            left = self.deadline - time.time()
+            if left <= 0:
+                why = (f"hard deadline: {self.deadline - T_START:.0f} s after start, still in leg "
+                       f"{self.d.leg or '(between legs)'}")
+                break
+            ready, _, _ = select.select([self._r], [], [], left)
+            if ready:
+                os.read(self._r, 64)
+                why = (f"terminated by the launcher (SIGTERM: another rank exited) in leg "
+                       f"{self.d.leg or '(between legs)'}")
+                break
+        if self.rank == 0:
+            self.emit(error=why)
+        os._exit(0)
+
+    def update(self, **kv):
+        with self.lock:
+            self.data.update(kv)
+
+    def set_leg(self, name: str, res, info):
+        with self.lock:
+            self.data[name] = res if info is None else info
+
+    def emit(self, error: str | None = None):
+        """Print the line once (rank 0). Main thread and watchdog race safely:
+        the lock serialises them and the second caller finds `printed`."""
+        if self.rank != 0:
+            return
+        with self.lock:
+            if self.printed:
+                return
+            self.printed = True
+            line = dict(self.data)
+            if error:
+                line["error"] = error
+            # every leg that has no measurement in the line: failed, skipped, or cut off by `error`
+            bad = [x for x in LEG_NAMES if isinstance(line.get(x), dict)
+                   and ("error" in line[x] or "skipped" in line[x])]
+            if "main_error" in line or line.get("value") is None and not line.get("dry_run"):
+                bad = ["main"] + bad
+            if error and self.d.leg:
+                bad.append(self.d.leg)
+            line["legs_not_measured"] = bad
+            line["leg_seconds"] = dict(self.d.leg_seconds)
+            sys.stdout.write(json.dumps(line, default=str) + "\n")
+            sys.stdout.flush()
 
 
 def plan(args, d: Dist, free_bytes: int, parity_num: int, fill: bool = False) -> dict:
@@ -308,15 +553,16 @@ def host_cpu_model() -> str:
     return platform.processor() or platform.machine()
 
 
-def cpu_stripe(args, k, m, r, B, threads_list, seconds, literal=False, repair=True, seed=None):
+def cpu_stripe(args, k, m, r, B, threads_list, seconds, literal=False, repair=True, seed=None, kind="avx2"):
     """One whole stripe of CL(k, r, m) B-byte blocks through the reference's CPU
     flow, restated (oracle: test infrastructure, never the product): ECWide-C
-    encodeData = ec_encode_data with the AVX2 4-bit-split dot products (global
-    rows) + one pass per local group (NativeCodec.cc:137-219), then (repair)
-    decodeData of D0 = ec_encode_data of the r survivors with the all-ones
-    table (NativeCodec.cc:237-248), both split by byte range over `threads`
-    threads. GB/s (algorithmic bytes: inputs + outputs) per thread count, each
-    timed for about seconds / len(threads_list) (at least one whole stripe)."""
+    encodeData = ec_encode_data (kernel family `kind`: ISA-L 2.14's AVX2, or
+    master's AVX-512 / AVX-512 + GFNI) for the global rows + one pass per local
+    group (NativeCodec.cc:137-219), then (repair) decodeData of D0 =
+    ec_encode_data of the r survivors with the all-ones table
+    (NativeCodec.cc:237-248), both split by byte range over `threads` threads.
+    GB/s (algorithmic bytes: inputs + outputs) per thread count, each timed for
+    about seconds / len(threads_list) (at least one whole stripe)."""
     import ctypes
 
     import numpy as np
@@ -333,16 +579,17 @@ def cpu_stripe(args, k, m, r, B, threads_list, seconds, literal=False, repair=Tr
     pp = (u8p * len(par))(*[x.ctypes.data_as(u8p) for x in par])
     nsrc = min(r, k)
     per_stripe = (k + oc.parity_num + ((nsrc + 1) if repair else 0)) * B
-    ones = orc.init_tables(nsrc, 1, np.ones(nsrc, np.uint8))
+    ones = orc.init_tables_kind(kind, nsrc, 1, np.ones(nsrc, np.uint8))
     rep = np.zeros(B, np.uint8)
     rp = (u8p * 1)(rep.ctypes.data_as(u8p))
     srcs = data[1:nsrc] + [par[m]]
     sp = (u8p * nsrc)(*[x.ctypes.data_as(u8p) for x in srcs])
+    kid = oracle.KINDS[kind]
 
     def run(threads):
-        oc.encode_into(dp, pp, B, literal=literal, threads=threads)
+        oc.encode_into(dp, pp, B, literal=literal, threads=threads, kind=kind)
         if repair:
-            orc.L.orc_encode_data_avx2_mt(B, nsrc, 1, ones.ctypes.data_as(u8p), sp, rp, threads)
+            orc.L.orc_encode_data_mt_kind(kid, B, nsrc, 1, ones.ctypes.data_as(u8p), sp, rp, threads)
 
     run(max(threads_list))  # warm: fault in the output pages outside the timing
     res = {}
@@ -372,38 +619,76 @@ def cpu_meta(orc=None) -> dict:
         affinity = os.cpu_count()
     return {"cores_all": host_threads(), "affinity_cores": affinity, "nproc": os.cpu_count(),
             "cap": 16, "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "host_cpu": host_cpu_model(),
-            "avx2": (orc or oracle.Oracle()).have_avx2()}
+            "isa": {x: (orc or oracle.Oracle()).have_kind(x) for x in ("avx2", "avx512", "gfni")}}
+
+
+ISAL_FAMILY = {
+    "avx2": "ISA-L 2.14's gf_Nvect_dot_prod_avx2 (4-bit split vpshufb, 32-byte vectors): the top of the 2.14 tarball "
+            "ECWide-H bundles (isal:erasure_code/ec_multibinary.asm:119-135)",
+    "avx512": "ISA-L master's gf_Nvect_dot_prod_avx512 (4-bit split vpshufb, 64-byte vectors)",
+    "gfni": "ISA-L master's gf_Nvect_dot_prod_avx512_gfni (one vgf2p8affineqb per source byte and row, "
+            "ec_init_tables_gfni 8-byte matrices)",
+    "base": "ec_encode_data_base (scalar)",
+}
 
 
 def cpu_baseline(args, k, m, r, B):
-    """The headline workload's CPU baseline (rank 0, N=1): one whole stripe,
-    1 thread (ECWide-C's one ComputeWorker thread) as `value`, and the thread
-    scaling 1 -> 2 -> 4 -> 8 -> the box's per-GPU CPU share (16: the pool's
-    limit for one GPU's job, OMP_NUM_THREADS there) as `value_all_cores`."""
+    """The headline workload's CPU baseline (rank 0, N=1): one whole stripe
+    through the reference's CPU flow in three kernel families. `value` is the
+    family ISA-L master's dispatch picks on this host -- ECWide-C as built
+    (ECWide-C/makefile:12-14 links /usr/lib/libisal.so from unpinned master,
+    ECWide-C/README.md:34-39): AVX-512 + GFNI on the box's Zen 5 -- on 1 thread
+    (ECWide-C's one ComputeWorker thread), with the thread scaling 1 -> 2 ->
+    4 -> 8 -> the box's per-GPU CPU share (16). The other families (ISA-L
+    2.14's AVX2 = what ECWide-H's tarball builds; master's AVX-512 without
+    GFNI) at 1 and 16 threads beside it."""
     from ecwide_amd.shard import host_threads
 
+    import oracle
+
+    orc = oracle.Oracle()
+    master = orc.isal_master_kind()
     allc = host_threads()
     tl = sorted({t for t in (1, 2, 4, 8) if t < allc} | {allc})
-    res, ok = cpu_stripe(args, k, m, r, B, tl, args.cpu_seconds)
+    res, ok = cpu_stripe(args, k, m, r, B, tl, args.cpu_seconds, kind=master)
     if not ok:
         raise SystemExit("CPU baseline repair mismatch")
     per_thread = {t: round(v / t, 3) for t, v in res.items()}
-    return {
+    fam = {master: {"1": res[1], str(allc): res[allc]}}
+    for kind in ("avx2", "avx512", "gfni"):
+        if kind != master and orc.have_kind(kind):
+            rk, ok = cpu_stripe(args, k, m, r, B, sorted({1, allc}), args.cpu_seconds / 2, kind=kind)
+            if not ok:
+                raise SystemExit(f"CPU baseline repair mismatch ({kind})")
+            fam[kind] = {"1": rk[1], str(allc): rk[allc]}
+    out = {
         "value": res[1],
         "unit": "GB/s",
         "cores": 1,
         "kind": "port",
+        "isal_family": master,
         "sample": (f"1 whole stripe of the workload, CL(k={k},r={r},m={m}) B={B >> 20} MiB: ECWide-C encodeData "
-                   f"flow (AVX2 nibble-pshufb port of ISA-L's gf_Nvect_dot_prod_avx2, global + per-group passes) "
-                   f"+ decodeData of D0; 1 thread = ECWide-C's one ComputeWorker thread"),
+                   f"flow (global + per-group ec_encode_data passes) + decodeData of D0, on "
+                   f"{ISAL_FAMILY[master]}; 1 thread = ECWide-C's one ComputeWorker thread"),
+        "dispatch_rule": ("ISA-L master's ec_encode_data / ec_init_tables dispatch: AVX-512 (F+BW) + GFNI -> "
+                          "avx512_gfni, else AVX-512 -> avx512, else AVX2 -> avx2; ISA-L 2.14 stops at AVX2. "
+                          f"This host: {master}"),
         "value_all_cores": res[allc],
         "thread_scaling_GBps": {str(t): v for t, v in res.items()},
         "per_thread_GBps": {str(t): v for t, v in per_thread.items()},
+        "families_GBps": fam,
+        "ecwide_c_as_built": f"{master} (value, value_all_cores)",
+        "ecwide_h_isal_2_14": "avx2 (families_GBps.avx2)",
         "all_cores_note": (f"{allc} threads = this job's CPU share on the GPU box (the pool gives one GPU's job 16 of "
                            f"the host's CPUs and caps worker pools there); the host has more cores, which other "
                            f"jobs use"),
-        **cpu_meta(),
+        **cpu_meta(orc),
     }
+    for kind in ("avx2", "avx512", "gfni"):
+        if kind in fam:
+            out[f"value_{kind}"] = fam[kind]["1"]
+            out[f"value_{kind}_all_cores"] = fam[kind][str(allc)]
+    return out
 
 
 # ---- verification (outside the timed region) ---------------------------------
@@ -657,10 +942,11 @@ def chunkgen_leg(args, cpu_seconds: float = 0.0) -> dict:
         if cpu_seconds > 0:
             # the reference's own configs[0] timing on this host: encodeChunks on the CPU, i.e. encodeData of
             # the same 64 MiB chunks, literal mode, no repair (ChunkGenerator.java:126-131), one thread
+            fam = oracle.Oracle().isal_master_kind()  # ECWide-C as built (ISA-L master's dispatch here)
             res, _ = cpu_stripe(args, scheme.k, scheme.globalParityNum, scheme.groupDataNum, B, [1], cpu_seconds,
-                                literal=True, repair=False, seed=args.seed)
+                                literal=True, repair=False, seed=args.seed, kind=fam)
             cpu = {"encodeChunks_GBps": res[1], "encodeChunks_ms": round(nb * B / (res[1] * 1e9) * 1e3, 1),
-                   "cores": 1, "kind": "port",
+                   "cores": 1, "kind": "port", "isal_family": fam,
                    "sample": "encodeData of one stripe of the default scheme.ini's 64 MiB chunks (literal L), "
                              "ECWide-C's one ComputeWorker thread"}
         return {
@@ -862,67 +1148,70 @@ def ecwide_h_sequence(args, shim, orc, ln: int) -> dict:
 
 
 # ---- the bench ------------------------------------------------------------------
-def dry_run(args, d: Dist):
-    """The N>1 orchestration without a GPU: both legs' plans, a stand-in timed
-    region (each rank sleeps a rank-dependent time), the same reductions, and
-    the line's `config` built exactly as the real run builds it."""
+def dry_main(args, d: Dist) -> dict:
+    """The main leg without a GPU (--dry-run: the CPU test of the N>1 path):
+    the leg's plan, a stand-in timed region (each rank sleeps a rank-dependent
+    time) between the same barriers, the same reductions, and the line's
+    `config` built exactly as the real run builds it."""
     k, m, r = args.k, args.m, args.r
     g = -(-k // r)
-    free = int(args.dry_run_free_gib * (1 << 30))
-    pl = plan(args, d, free, m + g, fill=args.hbm_fill)
+    pl = plan(args, d, int(args.dry_run_free_gib * (1 << 30)), m + g, fill=args.hbm_fill)
     sh = pl["share"]
     enc_bytes = sh["stripes"] * (k + m + g) * sh["block_bytes"]
     rep_bytes = sh["stripes"] * (min(r, k) + 1) * sh["block_bytes"]
-    d.barrier()
-    t0 = time.perf_counter()
-    time.sleep(0.05 * (1 + d.rank))
-    d.barrier()
-    el = time.perf_counter() - t0
+    el = dry_timed(d, 0.05)
     el_max = d.reduce(el, "max")
     shares = [d.gather(float(sh[key])) for key in ("s0", "stripes", "block_bytes", "col_offset")]
     per_rank = d.gather(el)
     steps = max(1, args.steps)
-    c4 = None
-    if args.configs4_steps > 0 and not args.hbm_fill:
-        p4 = plan(args, d, free, m + g, fill=True)
-        c4 = {"stripes_total": p4["stripes_total"], "block_bytes": p4["block_bytes_full"],
-              "stripes_per_gpu": p4["share"]["stripes"],
-              "rank_ms_per_step": [round(x / args.configs4_steps * 1e3, 4) for x in d.gather(el)],
-              "shares": [dict(s0=int(a), stripes=int(b)) for a, b in
-                         zip(*[d.gather(float(p4["share"][key])) for key in ("s0", "stripes")])]}
-    shapes = {}
-    if args.shape_steps > 0 and not args.hbm_fill and not args.strong:
-        for name, _, sk, sm, sr, mib, stripes, seed in SHAPE_LEGS:
-            a = argparse.Namespace(**vars(args))
-            a.k, a.m, a.r, a.block_mib, a.stripes, a.seed, a.strong = sk, sm, sr, float(mib), stripes, seed, False
-            ps = plan(a, d, free, sm + -(-sk // sr))
-            shapes[name] = {"stripes_per_gpu": ps["share"]["stripes"], "stripes_total": ps["stripes_total"],
-                            "block_bytes": ps["block_bytes_full"],
-                            "rank_ms_per_step": [round(x / args.shape_steps * 1e3, 4) for x in d.gather(el)]}
-    d.barrier()  # the host legs start after every rank's timed legs
-    host = None
-    if args.host_iters > 0:
-        # the per-rank host-resident leg's orchestration: every rank between two
-        # barriers, the same gathers as host_resident_leg (no GPU: no pinning)
-        d.barrier()
-        t0 = time.perf_counter()
-        time.sleep(0.01 * (1 + d.rank))
-        d.barrier()
-        hel = d.reduce(time.perf_counter() - t0, "max")
-        host = {"el_max": hel, "rank_GBps": d.gather(0.0), "rank_h2d_GBps": d.gather(0.0),
-                "rank_numa_node": [int(x) for x in d.gather(-1.0)],
-                "rank_gpu_numa_node": [int(x) for x in d.gather(-1.0)]}
-    if d.rank == 0:
-        print(json.dumps({"dry_run": True, "n_gpus": d.world, "scaling": "strong" if pl["strong"] else "weak",
-                          "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
-                          "block_bytes": pl["block_bytes_full"], "el_max": el_max, "rank_seconds": per_rank,
-                          "rank_ms_per_step": [round(x / steps * 1e3, 4) for x in per_rank],
-                          "roofline": {"rank_launch_ms": [round(x * 1e3 / steps, 4) for x in per_rank]},
-                          "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
-                          "configs4": c4, **shapes, "host_resident": host,
-                          "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
-                                     for a, b, c, o in zip(*shares)]}), flush=True)
-    d.close()
+    return {"metric": METRIC, "value": None, "unit": "GB/s", "dry_run": True, "n_gpus": d.world,
+            "scaling": "strong" if pl["strong"] else "weak",
+            "hbm_fill": pl["hbm_fill"], "stripes_total": pl["stripes_total"],
+            "block_bytes": pl["block_bytes_full"], "el_max": el_max, "rank_seconds": per_rank,
+            "rank_ms_per_step": [round(x / steps * 1e3, 4) for x in per_rank],
+            "roofline": {"rank_launch_ms": [round(x * 1e3 / steps, 4) for x in per_rank]},
+            "config": config_of(args, pl, k, m, r, g, d.world, enc_bytes, rep_bytes),
+            "shares": [dict(s0=int(a), stripes=int(b), block_bytes=int(c), col_offset=int(o))
+                       for a, b, c, o in zip(*shares)]}
+
+
+def dry_timed(d: Dist, unit_s: float) -> float:
+    d.barrier()
+    t0 = time.perf_counter()
+    time.sleep(unit_s * (1 + d.rank))
+    d.barrier()
+    return time.perf_counter() - t0
+
+
+def dry_configs4(args, d: Dist) -> dict:
+    k, m, r = args.k, args.m, args.r
+    p4 = plan(args, d, int(args.dry_run_free_gib * (1 << 30)), m + -(-k // r), fill=True)
+    el = dry_timed(d, 0.02)
+    return {"stripes_total": p4["stripes_total"], "block_bytes": p4["block_bytes_full"],
+            "stripes_per_gpu": p4["share"]["stripes"],
+            "rank_ms_per_step": [round(x / args.configs4_steps * 1e3, 4) for x in d.gather(el)],
+            "shares": [dict(s0=int(a), stripes=int(b)) for a, b in
+                       zip(*[d.gather(float(p4["share"][key])) for key in ("s0", "stripes")])]}
+
+
+def dry_shape(args, d: Dist, leg_def) -> dict:
+    name, _, sk, sm, sr, mib, stripes, seed = leg_def
+    a = argparse.Namespace(**vars(args))
+    a.k, a.m, a.r, a.block_mib, a.stripes, a.seed, a.strong = sk, sm, sr, float(mib), stripes, seed, False
+    ps = plan(a, d, int(args.dry_run_free_gib * (1 << 30)), sm + -(-sk // sr))
+    el = dry_timed(d, 0.01)
+    return {"stripes_per_gpu": ps["share"]["stripes"], "stripes_total": ps["stripes_total"],
+            "block_bytes": ps["block_bytes_full"],
+            "rank_ms_per_step": [round(x / args.shape_steps * 1e3, 4) for x in d.gather(el)]}
+
+
+def dry_host(args, d: Dist) -> dict:
+    """host_resident_leg's orchestration: every rank between two barriers,
+    the same gathers (no GPU: no pinning)."""
+    hel = d.reduce(dry_timed(d, 0.01), "max")
+    return {"el_max": hel, "rank_GBps": d.gather(0.0), "rank_h2d_GBps": d.gather(0.0),
+            "rank_numa_node": [int(x) for x in d.gather(-1.0)],
+            "rank_gpu_numa_node": [int(x) for x in d.gather(-1.0)], "verified": bool(d.reduce(1.0, "min"))}
 
 
 def device_leg(args, d: Dist, E, pl: dict, k: int, m: int, r: int, steps: int, warmup: int, layout: str) -> dict:
@@ -998,6 +1287,46 @@ def pmc_traffic(args, k, r, m, B, S, enc_bytes, launches):
         return ratio * enc_bytes / launches, src
     except Exception:
         return None, None
+
+
+def read_kernel_stats(path: str) -> list:
+    """Rows of a rocprofv3 --stats kernel summary (…_kernel_stats.csv):
+    (name, calls, average ns)."""
+    import csv
+
+    with open(path, newline="") as f:
+        return [(row["Name"], int(row["Calls"]), float(row["AverageNs"])) for row in csv.DictReader(f)]
+
+
+def profile_fracs(args, enc_bytes_per_launch: int, rep_bytes_per_launch: int) -> dict:
+    """The roofline recomputed from the committed rocprof summary of this
+    workload (--profile-csv): algorithmic bytes per launch / the kernel's
+    average rocprof duration / 8 TB/s, for the encode (the most-called
+    encode_kernel row) and the repair (the most-called xor_kernel row). Only
+    at the default workload, the one the summary was taken on."""
+    default = (args.k, args.m, args.r, args.block_mib or 64.0, args.stripes or 8, args.layout, args.chunk_kib or 8,
+               args.unit_pad, args.hbm_fill, args.strong) == (128, 3, 27, 64.0, 8, "tiled", 8, 0, False, False)
+    rel = os.path.relpath(args.profile_csv, REPO)
+    if not default or not os.path.exists(args.profile_csv):
+        return {"profile_source": None, "profile_note": f"{rel}: " + ("absent" if default else
+                                                                       "taken on the default workload only")}
+    rows = read_kernel_stats(args.profile_csv)
+
+    def pick(tag):
+        c = [x for x in rows if tag in x[0]]
+        return max(c, key=lambda x: x[1]) if c else None
+
+    enc, rep = pick("encode_kernel"), pick("xor_kernel")
+    out = {"profile_source": rel}
+    if enc:
+        out.update(profile_encode_kernel=enc[0], profile_encode_calls=enc[1],
+                   profile_launch_ms=round(enc[2] / 1e6, 4),
+                   profile_frac=round(enc_bytes_per_launch / (enc[2] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4))
+    if rep:
+        out.update(profile_repair_kernel=rep[0], profile_repair_calls=rep[1],
+                   profile_repair_launch_ms=round(rep[2] / 1e6, 4),
+                   profile_repair_frac=round(rep_bytes_per_launch / (rep[2] * 1e-9) / 1e9 / HBM_PEAK_GBS, 4))
+    return out
 
 
 def configs4_leg(args, d: Dist, E, k, m, r) -> dict:
@@ -1088,45 +1417,37 @@ def shape_leg(args, d: Dist, E, leg_def) -> dict:
 
 def shape_cpu_baseline(args, leg_def) -> dict:
     """A SHAPE_LEGS entry's CPU baseline: one whole stripe of that shape through
-    the same encodeData + decodeData flow as the headline's, 1 thread (and the
-    box's per-GPU share)."""
+    the same encodeData + decodeData flow as the headline's, on the family
+    ISA-L master picks here (ECWide-C as built) and on 2.14's AVX2, 1 thread
+    and the box's per-GPU share."""
     from ecwide_amd.shard import host_threads
 
+    import oracle
+
     name, desc, k, m, r, mib, stripes, seed = leg_def
+    master = oracle.Oracle().isal_master_kind()
     allc = host_threads()
-    res, ok = cpu_stripe(args, k, m, r, int(mib) << 20, sorted({1, allc}), args.cpu_seconds / 3, seed=seed)
-    return {"value": res[1], "unit": "GB/s", "cores": 1, "kind": "port", "value_all_cores": res[allc],
-            "cores_all": allc, "verified": bool(ok),
+    res, ok = cpu_stripe(args, k, m, r, int(mib) << 20, sorted({1, allc}), args.cpu_seconds / 3, seed=seed,
+                         kind=master)
+    r2, ok2 = cpu_stripe(args, k, m, r, int(mib) << 20, sorted({1, allc}), args.cpu_seconds / 4, seed=seed,
+                         kind="avx2")
+    return {"value": res[1], "unit": "GB/s", "cores": 1, "kind": "port", "isal_family": master,
+            "value_all_cores": res[allc], "value_avx2": r2[1], "value_avx2_all_cores": r2[allc],
+            "cores_all": allc, "verified": bool(ok and ok2),
             "sample": f"1 whole stripe of CL(k={k},r={r},m={m}) B={mib} MiB: encodeData flow + decodeData of D0"}
 
 
-def main():
-    argv = sys.argv[1:]
-    args = parse(argv)
-    if args.gpus < 1:
-        raise SystemExit("--gpus must be >= 1")
-    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
-        # decide before anything touches the GPU; the ranks are fresh processes
-        sys.exit(spawn_ranks(args.gpus, argv))
-    if args.host_resident:
-        host_resident(args)
-        return
-    if args.small_calls:
-        small_calls(args)
-        return
-    d = Dist(args)
-    if args.dry_run:
-        dry_run(args, d)
-        return
+def main_leg(args, d: Dist, E, ctx: dict) -> dict:
+    """The headline leg: this rank's share of the metric's workload, timed,
+    verified; returns the line's main fields (ctx keeps the slab for the
+    other_layout leg)."""
     import torch
-
-    import ecwide_amd as E
 
     k, m, r = args.k, args.m, args.r
     g = -(-k // r)
     pl = plan(args, d, torch.cuda.mem_get_info(d.dev)[0], m + g, fill=args.hbm_fill)
     leg = device_leg(args, d, E, pl, k, m, r, args.steps, args.warmup, args.layout)
-    codec, slab, out = leg["codec"], leg["slab"], leg["out"]
+    slab, out = leg["slab"], leg["out"]
     enc_bytes, rep_bytes = leg["enc_bytes"], leg["rep_bytes"]
     sh = pl["share"]
     B, S = sh["block_bytes"], sh["stripes"]
@@ -1143,8 +1464,8 @@ def main():
     enc_ms, rep_ms = leg["enc_ms_max"], leg["rep_ms_max"]
     achieved = enc_bytes / (enc_ms * 1e-3) / 1e9
     traffic, traffic_src = pmc_traffic(args, k, r, m, B, S, enc_bytes, launches)
-    line = {
-        "metric": "device-resident encode + single-block-repair GB/s, wide stripe (shards in HBM)",
+    fields = {
+        "metric": METRIC,
         "value": round(value, 2),
         "unit": "GB/s",
         "n_gpus": d.world,
@@ -1181,42 +1502,154 @@ def main():
             "launches_per_encode": launches,
             "encode_call_ms": round(enc_ms, 4),
             "repair_launch_ms": round(rep_ms, 4),
+            "repair_algorithmic_bytes_per_launch": rep_bytes,
             "repair_frac": round(rep_bytes / (rep_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+            **profile_fracs(args, enc_bytes // launches, rep_bytes),
         },
         "cpu_baseline": None,
     }
     if vres is not None:
-        line["verified"] = bool(ok_all)
-        line["verify"] = {key: vres[key] for key in ("windows", "repairs", "digests")} | (
+        fields["verified"] = bool(ok_all)
+        fields["verify"] = {key: vres[key] for key in ("windows", "repairs", "digests")} | (
             {"failed": vres["failed"]} if not vres["ok"] else {})
-    if d.world == 1 and args.other_layout_steps > 0 and args.other_layout_rounds > 0 and not pl["hbm_fill"]:
-        line["other_layout"] = other_layouts(args, E, codec, slab, S, B, out, enc_bytes, rep_bytes, d.dev)
-    del leg, slab, out, codec
-    torch.cuda.empty_cache()
-    if args.configs4_steps > 0 and not pl["hbm_fill"]:
-        line["configs4"] = configs4_leg(args, d, E, k, m, r)
-    if args.shape_steps > 0 and not pl["hbm_fill"] and not args.strong:
-        for leg_def in SHAPE_LEGS:
-            line[leg_def[0]] = shape_leg(args, d, E, leg_def)
-    d.barrier()  # the host legs below never overlap another rank's device-resident timed region
-    if args.host_iters > 0:
-        # every rank at once: the node's PCIe links and host DRAM together
-        line["host_resident"] = host_resident_leg(args, d, args.host_iters)
-    d.barrier()
+    ctx.update(codec=leg["codec"], slab=slab, out=out, S=S, B=B, enc_bytes=enc_bytes, rep_bytes=rep_bytes,
+               hbm_fill=pl["hbm_fill"])
+    return fields
+
+
+METRIC = "device-resident encode + single-block-repair GB/s, wide stripe (shards in HBM)"
+
+# Legs of one run, in order; all but `main` are optional (time budget) and none
+# can take the line down with it (Dist.run_leg). cpu_baseline and
+# chunk_generator run on rank 0 alone.
+LEG_NAMES = ("main", "other_layout", "configs4", "configs1", "configs0_shape", "host_resident", "cpu_baseline",
+             "chunk_generator")
+
+
+def leg_estimates(args, world: int) -> dict:
+    """Seconds each optional leg takes on an MI355X box (the round-5/6 driver
+    lines' leg_seconds, rounded up): what the time budget checks before it
+    starts a leg."""
+    c = max(0.0, args.cpu_seconds)
+    return {
+        "other_layout": 25.0 if world == 1 else 0.0,
+        "configs4": 40.0,            # fill + time + verify a ~280 GB slab
+        "configs1": 12.0, "configs0_shape": 12.0,
+        "host_resident": 25.0 + 3.0 * world,  # pinned NUMA-local staging of 8.6 GiB per rank
+        "cpu_baseline": (c * (1 + 2 / 2 + 2 * (1 / 3 + 1 / 4)) + 15.0) if world == 1 else 0.0,
+        "chunk_generator": 20.0 + (c / 4 if world == 1 else 0.0),
+    }
+
+
+def run_legs(args, d: Dist, line: Line) -> int:
+    """Every leg of the run through Dist.run_leg; the line is filled as they
+    finish. Returns the exit code: 0 when the main leg measured `value`."""
+    est = leg_estimates(args, d.world)
+    startup = round(time.time() - T_START, 1)
+    enabled = {
+        "other_layout": (d.world == 1 and args.other_layout_steps > 0 and args.other_layout_rounds > 0
+                         and not args.hbm_fill and not d.dry),
+        "configs4": args.configs4_steps > 0 and not args.hbm_fill,
+        "configs1": args.shape_steps > 0 and not args.hbm_fill and not args.strong,
+        "configs0_shape": args.shape_steps > 0 and not args.hbm_fill and not args.strong,
+        "host_resident": args.host_iters > 0,
+        "cpu_baseline": args.cpu_seconds > 0 and d.world == 1,
+        "chunk_generator": args.host_iters > 0,
+    }
+    E = None
+    if not d.dry:
+        import ecwide_amd as E
+    ctx = {}
+    res, info = d.run_leg("main", (lambda: dry_main(args, d)) if d.dry else (lambda: main_leg(args, d, E, ctx)))
+    rc = 0
+    if info is None:
+        line.update(**res)
+    else:
+        rc = 1
+        line.update(metric=METRIC, value=None, unit="GB/s", n_gpus=d.world, main_error=info)
+    line.update(budget={
+        "budget_s": args.budget_s, "deadline_s": args.deadline_s, "collective_timeout_s": args.collective_timeout,
+        "startup_s": startup, "estimate_s": {x: est[x] for x in est if enabled[x]},
+        "estimated_total_s": round(startup + 20.0 + sum(est[x] for x in est if enabled[x]), 1)})
+    if enabled["other_layout"] and ctx:
+        c = ctx
+        line.set_leg("other_layout", *d.run_leg(
+            "other_layout", lambda: other_layouts(args, E, c["codec"], c["slab"], c["S"], c["B"], c["out"],
+                                                  c["enc_bytes"], c["rep_bytes"], d.dev), est["other_layout"]))
+    ctx.clear()
+    d._free_device()
+    k, m, r = args.k, args.m, args.r
+    if enabled["configs4"]:
+        line.set_leg("configs4", *d.run_leg("configs4", (lambda: dry_configs4(args, d)) if d.dry else
+                                            (lambda: configs4_leg(args, d, E, k, m, r)), est["configs4"]))
+    for leg_def in SHAPE_LEGS:
+        name = leg_def[0]
+        if enabled[name]:
+            line.set_leg(name, *d.run_leg(name, (lambda: dry_shape(args, d, leg_def)) if d.dry else
+                                          (lambda: shape_leg(args, d, E, leg_def)), est[name]))
+    if enabled["host_resident"]:
+        # every rank at once: the node's PCIe links and host DRAM together (after
+        # every rank's device-resident legs: run_leg's closing sync)
+        line.set_leg("host_resident", *d.run_leg(
+            "host_resident", (lambda: dry_host(args, d)) if d.dry else
+            (lambda: host_resident_leg(args, d, args.host_iters)), est["host_resident"]))
     if d.rank == 0:
-        # CPU baselines: rank 0 at N = 1 only (a bounded sample of each workload on this host's cores)
-        cpu_on = args.cpu_seconds > 0 and d.world == 1
-        if cpu_on:
-            line["cpu_baseline"] = cpu_baseline(args, k, m, r, B)
-            for leg_def in SHAPE_LEGS:
-                if leg_def[0] in line:
-                    line[leg_def[0]]["cpu_baseline"] = shape_cpu_baseline(args, leg_def)
+        # rank 0 alone, no collectives: the CPU baselines (N = 1: a bounded sample
+        # of each workload on this host's cores) and the ChunkGenerator replay
+        if enabled["cpu_baseline"]:
+            def cpu_all():
+                res = {"headline": cpu_baseline(args, k, m, r, int((args.block_mib or 64.0) * (1 << 20)))}
+                for leg_def in SHAPE_LEGS:
+                    if enabled[leg_def[0]]:
+                        res[leg_def[0]] = shape_cpu_baseline(args, leg_def)
+                return res
+
+            res, info = d.run_leg("cpu_baseline", (lambda: {"headline": {"dry_run": True}}) if d.dry else cpu_all,
+                                  est["cpu_baseline"], local=True)
+            if info is not None:
+                line.set_leg("cpu_baseline", None, info)
+            else:
+                line.update(cpu_baseline=res.pop("headline"))
+                with line.lock:
+                    for name, cb in res.items():
+                        if isinstance(line.data.get(name), dict) and "error" not in line.data[name]:
+                            line.data[name] = dict(line.data[name], cpu_baseline=cb)
         elif args.cpu_seconds > 0:
-            line["cpu_baseline_note"] = "measured at N = 1 only (BENCH); the same host CPU path at every N"
-        if args.host_iters > 0:
-            line["host_resident"]["chunk_generator"] = chunkgen_leg(args, args.cpu_seconds / 4 if cpu_on else 0.0)
-        print(json.dumps(line), flush=True)
-    d.close()
+            line.update(cpu_baseline_note="measured at N = 1 only (BENCH); the same host CPU path at every N")
+        if enabled["chunk_generator"]:
+            cs = args.cpu_seconds / 4 if enabled["cpu_baseline"] else 0.0
+            line.set_leg("chunk_generator", *d.run_leg(
+                "chunk_generator", (lambda: {"dry_run": True}) if d.dry else (lambda: chunkgen_leg(args, cs)),
+                est["chunk_generator"], local=True))
+    return rc
+
+
+def main():
+    argv = sys.argv[1:]
+    args = parse(argv)
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # decide before anything touches the GPU; the ranks are fresh processes
+        sys.exit(spawn_ranks(args.gpus, argv))
+    if args.host_resident:
+        host_resident(args)
+        return
+    if args.small_calls:
+        small_calls(args)
+        return
+    d = Dist(args)
+    line = Line(d, args.deadline_s)
+    rc = 1
+    try:
+        rc = run_legs(args, d, line)
+    except BaseException as e:  # noqa: BLE001 -- the line goes out whatever happened
+        line.update(error=f"{type(e).__name__}: {e}"[:600])
+        raise
+    finally:
+        line.emit()
+        d.close()
+    sys.exit(rc)
 
 
 if __name__ == "__main__":

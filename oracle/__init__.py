@@ -79,6 +79,19 @@ class Oracle:
         L.orc_fill_random_at.argtypes = [_u8p, c_size_t, c_size_t, c_uint64, c_uint32, c_uint32]
         L.orc_xor_blocks.argtypes = [_u8pp, c_int, _u8p, c_size_t]
         L.orc_have_avx2.restype = c_int
+        # ISA-L master's kernel families (KINDS): the CPU baseline as ECWide-C builds it
+        L.orc_encode_data_kind.argtypes = [c_int, c_int, c_int, c_int, _u8p, _u8pp, _u8pp]
+        L.orc_encode_data_mt_kind.argtypes = [c_int, c_int, c_int, c_int, _u8p, _u8pp, _u8pp, c_int]
+        L.orc_init_tables_kind.argtypes = [c_int, c_int, c_int, _u8p, _u8p]
+        L.orc_nc_encode_kind.argtypes = [c_void_p, _u8pp, _u8pp, c_int, c_int, c_int]
+        L.orc_nc_encode_mt_kind.argtypes = [c_void_p, _u8pp, _u8pp, c_int, c_int, c_int, c_int]
+        L.orc_gfni_matrix.restype = c_uint64
+        L.orc_gfni_matrix.argtypes = [c_uint8]
+        L.orc_gfni_affine_byte.restype = c_uint8
+        L.orc_gfni_affine_byte.argtypes = [c_uint64, c_uint8]
+        L.orc_have_kind.argtypes = [c_int]
+        L.orc_have_kind.restype = c_int
+        L.orc_isal_master_kind.restype = c_int
 
     # -- arithmetic ----------------------------------------------------
     def gf_mul(self, a: int, b: int) -> int:
@@ -110,6 +123,28 @@ class Oracle:
         f(ln, len(src), rows, tbls.ctypes.data_as(_u8p), _ptrs(src), _ptrs(out))
         return out
 
+    def init_tables_kind(self, kind: str, k: int, rows: int, a: np.ndarray) -> np.ndarray:
+        """ec_init_tables in kernel family `kind`'s format (32 B per coefficient,
+        8 B for "gfni": ec_init_tables_gfni)."""
+        a = np.ascontiguousarray(a, np.uint8).reshape(-1)
+        g = np.zeros(32 * k * rows, np.uint8)
+        self.L.orc_init_tables_kind(KINDS[kind], k, rows, a.ctypes.data_as(_u8p), g.ctypes.data_as(_u8p))
+        return g
+
+    def encode_data_kind(self, kind: str, tbls: np.ndarray, src: list, rows: int, threads: int = 1):
+        ln = src[0].size
+        out = [np.zeros(ln, np.uint8) for _ in range(rows)]
+        self.L.orc_encode_data_mt_kind(KINDS[kind], ln, len(src), rows, tbls.ctypes.data_as(_u8p), _ptrs(src),
+                                       _ptrs(out), threads)
+        return out
+
+    def have_kind(self, kind: str) -> bool:
+        return bool(self.L.orc_have_kind(KINDS[kind]))
+
+    def isal_master_kind(self) -> str:
+        """The family ISA-L master's ec_encode_data dispatch picks on this CPU."""
+        return {v: n for n, v in KINDS.items()}[self.L.orc_isal_master_kind()]
+
     def fill(self, length: int, seed: int, stripe: int, block: int, offset: int = 0) -> np.ndarray:
         """Bytes [offset, offset + length) of block `block` of stripe `stripe`
         (ecwide.h generator; offset a multiple of 8)."""
@@ -130,6 +165,10 @@ class Oracle:
               multinode: bool = False) -> "OracleCodec":
         return OracleCodec(self, code_type, k, m, r, chunk, node, multinode)
 
+
+# ec_encode_data kernel families: ISA-L 2.14's base and AVX2 (the tarball ECWide-H
+# bundles), and ISA-L master's AVX-512 and AVX-512 + GFNI (what ECWide-C links)
+KINDS = {"base": 0, "avx2": 1, "avx512": 2, "gfni": 3}
 
 FIELDS = ("encode_data_num", "decode_data_num", "partial_decode_num", "group_num",
           "rack_nodes_num", "rack_num", "rack_per_group", "group_data_num")
@@ -160,18 +199,22 @@ class OracleCodec:
         n = 32 * self.encode_data_num * self.m
         return np.ctypeslib.as_array(self.L.orc_codec_gftbl(self.h), (n,)).copy()
 
-    def encode(self, data: list, literal: bool = False, avx2: bool = False, threads: int = 0):
+    def encode(self, data: list, literal: bool = False, avx2: bool = False, threads: int = 0,
+               kind: str | None = None):
         ln = data[0].size
         par = [np.zeros(ln, np.uint8) for _ in range(self.parity_num)]
-        if threads:
+        if kind is not None:
+            self.L.orc_nc_encode_mt_kind(self.h, _ptrs(data), _ptrs(par), int(literal), max(1, threads), ln,
+                                         KINDS[kind])
+        elif threads:
             self.L.orc_nc_encode_mt(self.h, _ptrs(data), _ptrs(par), int(literal), threads, ln)
         else:
             self.L.orc_nc_encode_len(self.h, _ptrs(data), _ptrs(par), int(literal), int(avx2), ln)
         return par
 
-    def encode_into(self, dptrs, pptrs, ln: int, literal: bool = False, threads: int = 1):
+    def encode_into(self, dptrs, pptrs, ln: int, literal: bool = False, threads: int = 1, kind: str = "avx2"):
         """Raw-pointer form used by the bench's cpu_baseline leg."""
-        self.L.orc_nc_encode_mt(self.h, dptrs, pptrs, int(literal), threads, ln)
+        self.L.orc_nc_encode_mt_kind(self.h, dptrs, pptrs, int(literal), threads, ln, KINDS[kind])
 
     def decode(self, data: list) -> np.ndarray:
         out = np.zeros(data[0].size, np.uint8)

@@ -17,6 +17,18 @@
  *   ec_encode_data_avx2 dispatch ... isal:erasure_code/ec_highlevel_func.c:106-135
  *     + gf_Nvect_dot_prod_avx2 ..... isal:erasure_code/gf_3vect_dot_prod_avx2.asm:293-380
  *       (4-bit split vpshufb lookups; restated with intrinsics, same algorithm)
+ *   ISA-L master's AVX-512 and AVX-512+GFNI kernels, which the reference's
+ *   ECWide-C links (ECWide-C/makefile:12-14 -> /usr/lib/libisal.so, built from
+ *   unpinned ISA-L master per ECWide-C/README.md:34-39). NOT in
+ *   /root/reference: restated from ISA-L's published design (2.31+):
+ *     ec_encode_data_avx512 ..... gf_{1..6}vect_dot_prod_avx512: the same
+ *                                 4-bit split on 64-byte vectors, <= 6 rows a pass
+ *     ec_init_tables_gfni ....... one 8x8 GF(2) matrix (8 bytes) per coefficient
+ *     ec_encode_data_avx512_gfni  gf_Nvect_dot_prod_avx512_gfni: one
+ *                                 vgf2p8affineqb per source byte and row
+ *   Their arithmetic is pinned bit-exact against oracle/_ref (ISA-L 2.14's
+ *   ec_encode_data_base) by tests/test_oracle.py; their pass schedule is not
+ *   (no master source here) -- it only moves the CPU timing, not the bytes.
  *   NativeCodec field derivations .. ECWide-C/src/NativeCodec.java:20-109,145-195
  *   CodingScheme derivations ....... ECWide-C/src/CodingScheme.java:22-48
  *   generateEncodeMatrix ........... ECWide-C/src/native/NativeCodec.cc:12-64 (single-node branch)
@@ -179,6 +191,176 @@ void orc_encode_data_avx2(int len, int srcs, int dests, const uint8_t* v, uint8_
 #endif
 }
 
+/* ---- ISA-L master kernel families (CPU baseline "as ECWide-C builds it") ----
+ * kind: 0 = ec_encode_data_base, 1 = AVX2 (ISA-L 2.14's top), 2 = AVX-512BW
+ * (4-bit split vpshufb, 64-byte vectors), 3 = AVX-512 + GFNI (vgf2p8affineqb).
+ * Table format: 32 bytes per coefficient for kinds 0-2 (ec_init_tables), 8
+ * bytes for kind 3 (ec_init_tables_gfni). */
+enum { ORC_BASE = 0, ORC_AVX2 = 1, ORC_AVX512 = 2, ORC_GFNI = 3 };
+
+/* the 8x8 GF(2) matrix of x -> c*x (poly 0x11D) in vgf2p8affineqb's layout:
+ * result bit i = parity(x & byte[7 - i]) */
+uint64_t orc_gfni_matrix(uint8_t c) {
+  uint64_t m = 0;
+  for (int i = 0; i < 8; ++i) {
+    uint8_t row = 0;
+    for (int j = 0; j < 8; ++j)
+      if (orc_gf_mul(c, (uint8_t)(1u << j)) & (1u << i)) row |= (uint8_t)(1u << j);
+    m |= (uint64_t)row << (8 * (7 - i));
+  }
+  return m;
+}
+
+void orc_init_tables_gfni(int k, int rows, const uint8_t* a, uint8_t* g_tbls) {
+  for (int i = 0; i < rows * k; ++i) {
+    uint64_t m = orc_gfni_matrix(a[i]);
+    memcpy(g_tbls + 8 * (size_t)i, &m, 8);
+  }
+}
+
+/* scalar model of vgf2p8affineqb (imm8 = 0) on one byte: the checker of the
+ * matrix layout on a CPU without GFNI */
+uint8_t orc_gfni_affine_byte(uint64_t m, uint8_t x) {
+  uint8_t y = 0;
+  for (int i = 0; i < 8; ++i) {
+    uint8_t row = (uint8_t)(m >> (8 * (7 - i)));
+    y |= (uint8_t)((__builtin_popcount(row & x) & 1) << i);
+  }
+  return y;
+}
+
+#if defined(__x86_64__)
+__attribute__((target("avx512f,avx512bw"))) static void dot_prod_avx512_rows(int len, int srcs, int rows,
+                                                                             const uint8_t* v, uint8_t** src,
+                                                                             uint8_t** dest) {
+  const __m512i mask = _mm512_set1_epi8(0x0f);
+  int pos = 0;
+  for (;;) {
+    if (pos > len - 64) {
+      if (pos == len) break;
+      pos = len - 64; /* overlapping last vector */
+    }
+    __m512i acc[6];
+    for (int l = 0; l < rows; ++l) acc[l] = _mm512_setzero_si512();
+    for (int j = 0; j < srcs; ++j) {
+      __m512i x = _mm512_loadu_si512((const void*)(src[j] + pos));
+      __m512i lo = _mm512_and_si512(x, mask);
+      __m512i hi = _mm512_and_si512(_mm512_srli_epi64(x, 4), mask);
+      for (int l = 0; l < rows; ++l) {
+        const uint8_t* t = v + (size_t)l * srcs * 32 + (size_t)j * 32;
+        __m512i tl = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i*)t));
+        __m512i th = _mm512_broadcast_i32x4(_mm_loadu_si128((const __m128i*)(t + 16)));
+        acc[l] = _mm512_xor_si512(acc[l], _mm512_xor_si512(_mm512_shuffle_epi8(tl, lo),
+                                                           _mm512_shuffle_epi8(th, hi)));
+      }
+    }
+    for (int l = 0; l < rows; ++l) _mm512_storeu_si512((void*)(dest[l] + pos), acc[l]);
+    if (pos == len - 64) break;
+    pos += 64;
+  }
+}
+
+__attribute__((target("avx512f,avx512bw,gfni"))) static void dot_prod_gfni_rows(int len, int srcs, int rows,
+                                                                                const uint8_t* v, uint8_t** src,
+                                                                                uint8_t** dest) {
+  int pos = 0;
+  for (;;) {
+    if (pos > len - 64) {
+      if (pos == len) break;
+      pos = len - 64;
+    }
+    __m512i acc[6];
+    for (int l = 0; l < rows; ++l) acc[l] = _mm512_setzero_si512();
+    for (int j = 0; j < srcs; ++j) {
+      __m512i x = _mm512_loadu_si512((const void*)(src[j] + pos));
+      for (int l = 0; l < rows; ++l) {
+        uint64_t m;
+        memcpy(&m, v + 8 * ((size_t)l * srcs + j), 8);
+        acc[l] = _mm512_xor_si512(acc[l], _mm512_gf2p8affine_epi64_epi8(x, _mm512_set1_epi64((long long)m), 0));
+      }
+    }
+    for (int l = 0; l < rows; ++l) _mm512_storeu_si512((void*)(dest[l] + pos), acc[l]);
+    if (pos == len - 64) break;
+    pos += 64;
+  }
+}
+#endif
+
+int orc_have_kind(int kind) {
+#if defined(__x86_64__)
+  __builtin_cpu_init();
+  switch (kind) {
+    case ORC_BASE: return 1;
+    case ORC_AVX2: return __builtin_cpu_supports("avx2");
+    case ORC_AVX512: return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw");
+    case ORC_GFNI:
+      return __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512bw") &&
+             __builtin_cpu_supports("gfni");
+  }
+  return 0;
+#else
+  return kind == ORC_BASE;
+#endif
+}
+
+/* the kernel family ISA-L master's ec_encode_data dispatch picks on this CPU
+ * (ECWide-C as built): AVX-512 + GFNI, else AVX-512, else AVX2, else base */
+int orc_isal_master_kind(void) {
+  for (int kind = ORC_GFNI; kind > ORC_BASE; --kind)
+    if (orc_have_kind(kind)) return kind;
+  return ORC_BASE;
+}
+
+static void encode_data_base_gfni(int len, int srcs, int dests, const uint8_t* v, uint8_t** src, uint8_t** dest) {
+  for (int l = 0; l < dests; ++l)
+    for (int i = 0; i < len; ++i) {
+      uint8_t s = 0;
+      for (int j = 0; j < srcs; ++j) {
+        uint64_t m;
+        memcpy(&m, v + 8 * ((size_t)l * srcs + j), 8);
+        s ^= orc_gfni_affine_byte(m, src[j][i]);
+      }
+      dest[l][i] = s;
+    }
+}
+
+/* ec_encode_data of one kernel family; tables in that family's format */
+void orc_encode_data_kind(int kind, int len, int srcs, int dests, const uint8_t* v, uint8_t** src,
+                          uint8_t** dest) {
+  if (!orc_have_kind(kind)) kind = kind == ORC_GFNI ? -1 : ORC_BASE; /* -1: scalar model of the gfni tables */
+#if defined(__x86_64__)
+  if (kind == ORC_AVX2) {
+    orc_encode_data_avx2(len, srcs, dests, v, src, dest);
+    return;
+  }
+  if ((kind == ORC_AVX512 || kind == ORC_GFNI) && len >= 64) {
+    const int tb = kind == ORC_GFNI ? 8 : 32;
+    while (dests > 0) {
+      const int rows = dests < 6 ? dests : 6;
+      if (kind == ORC_GFNI)
+        dot_prod_gfni_rows(len, srcs, rows, v, src, dest);
+      else
+        dot_prod_avx512_rows(len, srcs, rows, v, src, dest);
+      v += (size_t)rows * srcs * tb;
+      dest += rows;
+      dests -= rows;
+    }
+    return;
+  }
+#endif
+  if (kind == ORC_GFNI || kind == -1)
+    encode_data_base_gfni(len, srcs, dests, v, src, dest);
+  else
+    orc_encode_data_base(len, srcs, dests, v, src, dest);
+}
+
+void orc_init_tables_kind(int kind, int k, int rows, const uint8_t* a, uint8_t* g_tbls) {
+  if (kind == ORC_GFNI)
+    orc_init_tables_gfni(k, rows, a, g_tbls);
+  else
+    orc_init_tables(k, rows, a, g_tbls);
+}
+
 /* ---------------- NativeCodec restatement ---------------- */
 typedef struct orc_codec {
   /* CodingScheme */
@@ -311,41 +493,52 @@ int orc_codec_field(const orc_codec* c, int which) {
 const uint8_t* orc_codec_matrix(const orc_codec* c) { return c->encode_matrix; }
 const uint8_t* orc_codec_gftbl(const orc_codec* c) { return c->encode_gftbl; }
 
-typedef void (*orc_ec_fn)(int, int, int, const uint8_t*, uint8_t**, uint8_t**);
-
-/* encodeData (NativeCodec.cc:137-219), single-node. `literal` reproduces
- * the zero local-parity tables (NativeCodec.cc:181-186); otherwise the
- * local tables are built from an all-ones row (the CL code as designed). */
-static void nc_encode(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
-                      orc_ec_fn ec, int off, int len) {
+/* encodeData (NativeCodec.cc:137-219), single-node, through the ec_encode_data
+ * of kernel family `kind`. `literal` reproduces the zero local-parity tables
+ * (NativeCodec.cc:181-186); otherwise the local tables are built from an
+ * all-ones row (the CL code as designed). */
+static void nc_encode(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int kind, int off,
+                      int len) {
   int k = c->encode_data_num, m = c->m;
   uint8_t* d[256];
   uint8_t* p[320];
   for (int j = 0; j < k; ++j) d[j] = data[j] + off;
   int np = m + ((c->code_type == 'C' || c->code_type == 'L') ? c->group_num : 0);
   for (int i = 0; i < np; ++i) p[i] = parity[i] + off;
-  ec(len, k, m, c->encode_gftbl, d, p);
+  if (kind == ORC_GFNI) {
+    uint8_t* g = (uint8_t*)malloc((size_t)8 * k * m + 8);
+    orc_init_tables_gfni(k, m, c->encode_matrix, g);
+    orc_encode_data_kind(kind, len, k, m, g, d, p);
+    free(g);
+  } else {
+    orc_encode_data_kind(kind, len, k, m, c->encode_gftbl, d, p);
+  }
   if (c->code_type != 'C' && c->code_type != 'L') return;
   int r = c->group_data_num;
   uint8_t row[256], *xor_tbl = (uint8_t*)malloc(32 * 256);
   memset(row, literal ? 0 : 1, sizeof row);
-  orc_init_tables(r, 1, row, xor_tbl);
+  orc_init_tables_kind(kind, r, 1, row, xor_tbl);
   int pos = m, offset = 0;
-  for (int t = 0; t < c->group_num - 1; ++t, ++pos, offset += r) ec(len, r, 1, xor_tbl, d + offset, p + pos);
+  for (int t = 0; t < c->group_num - 1; ++t, ++pos, offset += r)
+    orc_encode_data_kind(kind, len, r, 1, xor_tbl, d + offset, p + pos);
   int last = (k - 1) % r + 1;
-  orc_init_tables(last, 1, row, xor_tbl);
-  ec(len, last, 1, xor_tbl, d + offset, p + pos);
+  orc_init_tables_kind(kind, last, 1, row, xor_tbl);
+  orc_encode_data_kind(kind, len, last, 1, xor_tbl, d + offset, p + pos);
   free(xor_tbl);
 }
 
 void orc_nc_encode(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int avx2) {
-  nc_encode(c, data, parity, literal, avx2 ? orc_encode_data_avx2 : orc_encode_data_base, 0,
-            c->chunk_size);
+  nc_encode(c, data, parity, literal, avx2 ? ORC_AVX2 : ORC_BASE, 0, c->chunk_size);
 }
 
 void orc_nc_encode_len(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
                        int avx2, int len) {
-  nc_encode(c, data, parity, literal, avx2 ? orc_encode_data_avx2 : orc_encode_data_base, 0, len);
+  nc_encode(c, data, parity, literal, avx2 ? ORC_AVX2 : ORC_BASE, 0, len);
+}
+
+/* the same with an explicit kernel family (0 base, 1 AVX2, 2 AVX-512, 3 GFNI) */
+void orc_nc_encode_kind(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int kind, int len) {
+  nc_encode(c, data, parity, literal, kind, 0, len);
 }
 
 /* decodeData / partialDecodeData: ec_encode_data with the all-ones table */
@@ -374,29 +567,29 @@ void orc_nc_xor_intermediate(orc_codec* c, uint8_t** src, uint8_t** tgt, int len
   c->xori_called = 1;
 }
 
-/* ---- multi-threaded AVX2 baseline: the same flow split by byte range ---- */
+/* ---- multi-threaded CPU baseline: the same flow split by byte range ---- */
 typedef struct {
   const orc_codec* c;
   uint8_t** data;
   uint8_t** parity;
-  int literal, off, len;
+  int literal, off, len, kind;
 } mt_job;
 
 static void* mt_run(void* arg) {
   mt_job* j = (mt_job*)arg;
-  nc_encode(j->c, j->data, j->parity, j->literal, orc_encode_data_avx2, j->off, j->len);
+  nc_encode(j->c, j->data, j->parity, j->literal, j->kind, j->off, j->len);
   return NULL;
 }
 
-void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal,
-                      int nthreads, int len) {
+void orc_nc_encode_mt_kind(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int nthreads,
+                           int len, int kind) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   pthread_t th[256];
   mt_job jobs[256];
   int per = (len / nthreads) & ~63;
-  if (per < 64) {
-    nc_encode(c, data, parity, literal, orc_encode_data_avx2, 0, len);
+  if (nthreads == 1 || per < 64) {
+    nc_encode(c, data, parity, literal, kind, 0, len);
     return;
   }
   for (int t = 0; t < nthreads; ++t) {
@@ -404,6 +597,7 @@ void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int 
     jobs[t].data = data;
     jobs[t].parity = parity;
     jobs[t].literal = literal;
+    jobs[t].kind = kind;
     jobs[t].off = t * per;
     jobs[t].len = (t == nthreads - 1) ? len - t * per : per;
     pthread_create(&th[t], NULL, mt_run, &jobs[t]);
@@ -411,11 +605,16 @@ void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int 
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
 }
 
-/* ec_encode_data (AVX2 port) split by byte range over nthreads threads: the
- * multi-threaded form of decodeData / a CL repair (NativeCodec.cc:237-248:
- * ec_encode_data with the all-ones table) for the CPU baseline. */
+void orc_nc_encode_mt(const orc_codec* c, uint8_t** data, uint8_t** parity, int literal, int nthreads, int len) {
+  orc_nc_encode_mt_kind(c, data, parity, literal, nthreads, len, ORC_AVX2);
+}
+
+/* ec_encode_data (one kernel family) split by byte range over nthreads
+ * threads: the multi-threaded form of decodeData / a CL repair
+ * (NativeCodec.cc:237-248: ec_encode_data with the all-ones table) for the
+ * CPU baseline; tables in that family's format. */
 typedef struct {
-  int len, k, rows;
+  int len, k, rows, kind;
   const uint8_t* tbl;
   uint8_t* src[256];
   uint8_t* dst[256];
@@ -423,17 +622,17 @@ typedef struct {
 
 static void* ed_run(void* arg) {
   ed_job* j = (ed_job*)arg;
-  orc_encode_data_avx2(j->len, j->k, j->rows, j->tbl, j->src, j->dst);
+  orc_encode_data_kind(j->kind, j->len, j->k, j->rows, j->tbl, j->src, j->dst);
   return NULL;
 }
 
-void orc_encode_data_avx2_mt(int len, int k, int rows, const uint8_t* tbl, uint8_t** src, uint8_t** dst,
-                             int nthreads) {
+void orc_encode_data_mt_kind(int kind, int len, int k, int rows, const uint8_t* tbl, uint8_t** src,
+                             uint8_t** dst, int nthreads) {
   if (nthreads < 1) nthreads = 1;
   if (nthreads > 256) nthreads = 256;
   int per = (len / nthreads) & ~63;
   if (nthreads == 1 || per < 64 || k > 256 || rows > 256) {
-    orc_encode_data_avx2(len, k, rows, tbl, src, dst);
+    orc_encode_data_kind(kind, len, k, rows, tbl, src, dst);
     return;
   }
   pthread_t th[256];
@@ -443,6 +642,7 @@ void orc_encode_data_avx2_mt(int len, int k, int rows, const uint8_t* tbl, uint8
     jobs[t].len = (t == nthreads - 1) ? len - off : per;
     jobs[t].k = k;
     jobs[t].rows = rows;
+    jobs[t].kind = kind;
     jobs[t].tbl = tbl;
     for (int i = 0; i < k; ++i) jobs[t].src[i] = src[i] + off;
     for (int i = 0; i < rows; ++i) jobs[t].dst[i] = dst[i] + off;
@@ -450,6 +650,11 @@ void orc_encode_data_avx2_mt(int len, int k, int rows, const uint8_t* tbl, uint8
   }
   for (int t = 0; t < nthreads; ++t) pthread_join(th[t], NULL);
   free(jobs);
+}
+
+void orc_encode_data_avx2_mt(int len, int k, int rows, const uint8_t* tbl, uint8_t** src, uint8_t** dst,
+                             int nthreads) {
+  orc_encode_data_mt_kind(ORC_AVX2, len, k, rows, tbl, src, dst, nthreads);
 }
 
 /* ---------------- synthetic data (ecwide.h, ecw_fill_random_dev) ---------------- */

@@ -1,7 +1,11 @@
 """One rank of the 2-rank GPU test (tests/test_gpu_multirank.py), started by
 torch.distributed.run: the product's StripeSlab encode + D0 repair on this
 rank's share (ecwide_amd.shard.plan_rank) of a batch, written to
-<out>/rank<r>.npz for the parent to merge. Ranks may share one GPU (gloo)."""
+<out>/rank<r>.npz for the parent to merge. Each rank also checks its own
+share against the oracle (8 KiB column windows at the first and last piece of
+its column slice, first and last stripe; every D0 repair against the
+generator's bytes) and writes that verdict into the .npz, so two ranks that
+computed the same wrong bytes still fail. Ranks may share one GPU (gloo)."""
 import os
 import sys
 
@@ -35,9 +39,37 @@ def main():
     for s in range(sh["stripes"]):
         res[f"par{s}"] = np.stack([p.cpu().numpy() for p in slab.parity(s)])
         res[f"rep{s}"] = out[s * sh["block_bytes"]:(s + 1) * sh["block_bytes"]].cpu().numpy()
+    res.update(oracle_verdict(res, sh, k, m, r, chunk, seed))
     np.savez(os.path.join(outdir, f"rank{rank}.npz"), **res)
     dist.barrier()
     dist.destroy_process_group()
+
+
+def oracle_verdict(res, sh, k, m, r, W, seed) -> dict:
+    """This rank's share against the oracle (ECWide-C encodeData restated,
+    NativeCodec.cc:137-219): windows of W bytes at the first and last piece of
+    the column slice of the first and last stripe; D0 repairs against the
+    generator's own bytes of block 0."""
+    import oracle
+
+    orc = oracle.Oracle()
+    oc = orc.codec("C", k, m, r, W)
+    n, off0, s0 = sh["block_bytes"], sh["col_offset"], sh["s0"]
+    windows, bad = 0, []
+    for s in sorted({0, sh["stripes"] - 1}):
+        for off in sorted({0, n - W}):
+            want = oc.encode([orc.fill(W, seed, s0 + s, j, off0 + off) for j in range(k)])
+            for i, w in enumerate(want):
+                if not np.array_equal(res[f"par{s}"][i][off:off + W], w):
+                    bad.append(f"stripe {s0 + s} parity {i} column {off0 + off}")
+            windows += 1
+    repairs = 0
+    for s in range(sh["stripes"]):
+        if not np.array_equal(res[f"rep{s}"], orc.fill(n, seed, s0 + s, 0, off0)):
+            bad.append(f"stripe {s0 + s} D0 repair")
+        repairs += 1
+    return {"oracle_windows": windows, "oracle_repairs": repairs, "oracle_ok": not bad,
+            "oracle_failed": "; ".join(bad)}
 
 
 if __name__ == "__main__":

@@ -1,8 +1,9 @@
 """The N>1 path with the product on the GPU: two torch.distributed.run ranks
 (sharing the box's GPU, gloo) each encode and repair their share of a batch
-with StripeSlab (tests/mp_rank_worker.py); the union of their outputs equals
-the single-process encode of the whole batch, for stripe sharding and for the
-byte-column fallback."""
+with StripeSlab (tests/mp_rank_worker.py); each rank's share matches the
+oracle (its own verdict), and the union of their outputs equals the oracle's
+encode of the whole batch and the single-process GPU encode, for stripe
+sharding and for the byte-column fallback."""
 import os
 import socket
 import subprocess
@@ -42,6 +43,13 @@ def test_two_ranks_union_equals_single_process(tmp_path, mode):
     slab.encode()
     torch.cuda.synchronize()
     want = {s: np.stack([p.cpu().numpy() for p in slab.parity(s)]) for s in range(total)}
+    import oracle
+
+    orc = oracle.Oracle()
+    oc = orc.codec("C", k, m, r, B)  # ECWide-C encodeData restated (NativeCodec.cc:137-219)
+    want_orc = {s: np.stack(oc.encode([orc.fill(B, seed, s, j) for j in range(k)])) for s in range(total)}
+    for s in range(total):
+        assert np.array_equal(want[s], want_orc[s]), ("single-process GPU encode vs oracle", mode, s)
     d0 = {s: slab.block(s, 0).cpu().numpy() for s in range(total)}
     got_par = {s: np.zeros_like(want[s]) for s in range(total)}
     got_rep = {s: np.zeros(B, np.uint8) for s in range(total)}
@@ -49,6 +57,9 @@ def test_two_ranks_union_equals_single_process(tmp_path, mode):
     for rank in range(2):
         z = np.load(tmp_path / f"rank{rank}.npz")
         s0, off, n = int(z["s0"]), int(z["col_offset"]), int(z["stripes"])
+        # the rank's own check of its share against the oracle
+        assert bool(z["oracle_ok"]), (mode, rank, str(z["oracle_failed"]))
+        assert int(z["oracle_windows"]) >= 1 and int(z["oracle_repairs"]) == n, (mode, rank)
         for i in range(n):
             par, rep = z[f"par{i}"], z[f"rep{i}"]
             w = rep.size
@@ -58,5 +69,6 @@ def test_two_ranks_union_equals_single_process(tmp_path, mode):
             got_rep[s0 + i][off:off + w] = rep
     for s in range(total):
         assert covered[s].all(), (mode, s)
+        assert np.array_equal(got_par[s], want_orc[s]), (mode, s)
         assert np.array_equal(got_par[s], want[s]), (mode, s)
         assert np.array_equal(got_rep[s], d0[s]), (mode, s)

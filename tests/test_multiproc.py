@@ -158,7 +158,9 @@ def _bench(*args, env=None):
     e.update(env or {})
     p = subprocess.run([sys.executable, os.path.join(REPO, "bench.py"), *args], capture_output=True, text=True,
                        timeout=240, env=e)
-    return p, (json.loads(p.stdout.strip().splitlines()[-1]) if p.returncode == 0 else None)
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) <= 1, p.stdout[-2000:]  # rank 0 prints exactly one JSON line, whatever happened
+    return p, (json.loads(lines[0]) if lines else None)
 
 
 def test_bench_gpus2_launches_two_ranks_weak_default_and_configs4_leg():
@@ -238,7 +240,7 @@ def test_bench_dry_run_strong_and_column_modes():
     p, line = _bench("--gpus", "2", "--dry-run", "--hbm-fill")
     assert p.returncode == 0, p.stderr[-2000:]
     assert line["hbm_fill"] and line["scaling"] == "strong" and line["stripes_total"] == 256
-    assert line["configs4"] is None
+    assert line.get("configs4") is None
 
 
 def test_bench_rejects_world_size_mismatch():
@@ -258,3 +260,94 @@ def test_plan_rank_and_hbm_fill_sizing():
         assert [g["s0"] for g in got] == [256 // world * r for r in range(world)]
     w = plan_rank(8, 1 << 26, 4, 3, strong=False, per_rank=8)
     assert (w["s0"], w["stripes"]) == (24, 8)
+
+
+# ---- the fail-safe N>1 path: one JSON line whatever a rank does
+def _main_intact(line, n):
+    assert line["n_gpus"] == n and line["stripes_total"] == 8 * n and len(line["rank_seconds"]) == n
+    assert [x["s0"] for x in line["shares"]] == [8 * r for r in range(n)]
+
+
+@pytest.mark.parametrize("n,rank", [(8, 3), (2, 1)])
+def test_bench_injected_failure_in_host_leg(n, rank):
+    """A rank raising in the host-resident leg: every rank leaves that leg at
+    the same collective, the line carries host_resident.error with the rank,
+    the main leg and the other legs are intact, nobody hangs, rc 0."""
+    p, line = _bench("--gpus", str(n), "--dry-run", "--dry-run-fail", f"rank={rank},leg=host")
+    assert p.returncode == 0, p.stderr[-2000:]
+    _main_intact(line, n)
+    h = line["host_resident"]
+    assert h["rank"] == rank and h["failed_ranks"] == [rank] and "InjectedFailure" in h["error"]
+    assert line["legs_not_measured"] == ["host_resident"]
+    assert len(line["configs4"]["shares"]) == n and line["configs1"]["stripes_per_gpu"] == 32
+    assert line["chunk_generator"] == {"dry_run": True}  # rank 0's own leg after it still ran
+
+
+@pytest.mark.parametrize("n,rank,leg,at", [(8, 5, "configs4", 2), (2, 0, "configs1", 1), (2, 1, "main", 3)])
+def test_bench_injected_failure_mid_leg(n, rank, leg, at):
+    """The failing rank has passed some of the leg's collectives (at = the
+    collective it fails before) while the others wait in the next one: its
+    fail-sync stands in for that collective; the next leg runs normally."""
+    p, line = _bench("--gpus", str(n), "--dry-run", "--dry-run-fail", f"rank={rank},leg={leg},at={at}")
+    err = line["main_error"] if leg == "main" else line[leg]
+    assert err["rank"] == rank and f"before collective {at}" in err["error"]
+    assert line["legs_not_measured"] == [leg]
+    if leg == "main":
+        assert p.returncode == 1 and line["value"] is None  # no headline: a failed run
+        assert line["configs4"]["stripes_total"] == 256
+    else:
+        assert p.returncode == 0, p.stderr[-2000:]
+        _main_intact(line, n)
+        assert "stripes_total" in line["configs0_shape"] and "rank_GBps" in line["host_resident"]
+
+
+def test_bench_hung_rank_times_out_and_line_survives():
+    """A rank hanging inside a leg (as inside a GPU call): the others' leg
+    collective times out (--collective-timeout), they skip the later
+    collective legs, rank 0 prints the line; the hung rank exits at its
+    deadline, so the launcher returns."""
+    import time
+
+    t0 = time.time()
+    p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-fail", "rank=1,leg=configs1,at=1,mode=hang",
+                     "--collective-timeout", "4", "--deadline-s", "25")
+    assert time.time() - t0 < 120
+    assert p.returncode == 0, p.stderr[-2000:]
+    _main_intact(line, 2)
+    assert "collective failed in leg configs1" in line["configs1"]["error"]
+    for leg in ("configs0_shape", "host_resident"):
+        assert "no collectives after an earlier failure" in line[leg]["skipped"]
+    assert line["legs_not_measured"] == ["configs1", "configs0_shape", "host_resident"]
+    assert "configs4" in line and "error" not in line["configs4"]
+
+
+def test_bench_rank_exit_still_prints_line():
+    """A rank dying (segfault-like exit): torch.distributed.run SIGTERMs the
+    others; rank 0's watchdog prints what it has, naming the leg it was in."""
+    p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-fail", "rank=1,leg=configs4,at=1,mode=exit",
+                     "--collective-timeout", "20")
+    assert line is not None, p.stderr[-2000:]
+    _main_intact(line, 2)
+    assert "in leg configs4" in line["error"] and "configs4" in line["legs_not_measured"]
+
+
+def test_bench_time_budget_drops_optional_legs():
+    """--budget-s: a leg starts only if elapsed (max over ranks) + its
+    estimate fits; the decision is the same on every rank."""
+    p, line = _bench("--gpus", "2", "--dry-run", "--budget-s", "30")
+    assert p.returncode == 0, p.stderr[-2000:]
+    _main_intact(line, 2)
+    assert "time budget" in line["configs4"]["skipped"]  # 40 s estimate
+    assert "stripes_per_gpu" in line["configs1"]         # 12 s estimate fits
+    assert "configs4" in line["legs_not_measured"]
+
+
+def test_bench_n8_estimate_within_budget():
+    """The driver's 8-GPU run: every leg's estimate plus startup fits the
+    default budget, which sits below the hard deadline."""
+    p, line = _bench("--gpus", "8", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    b = line["budget"]
+    assert b["estimated_total_s"] < b["budget_s"] < b["deadline_s"] <= 540
+    assert set(b["estimate_s"]) == {"configs4", "configs1", "configs0_shape", "host_resident", "chunk_generator"}
+    assert line["legs_not_measured"] == []

@@ -158,3 +158,57 @@ def test_oracle_vs_ref_random_sweep(orc):
         for avx2 in (False, True):
             got = orc.encode_data(tb, data, m, avx2=avx2)
             assert all(np.array_equal(a, b) for a, b in zip(got, want)), (k, m, ln, avx2)
+
+
+# ---- ISA-L master's kernel families (the CPU baseline as ECWide-C builds it) ----
+def test_gfni_matrix_is_gf_mul(orc):
+    """The 8x8 GF(2) matrix of x -> c*x in vgf2p8affineqb's layout, checked
+    through the scalar model of the instruction for every (c, x)."""
+    rng = np.random.default_rng(3)
+    for c in range(256):
+        m = orc.L.orc_gfni_matrix(c)
+        for x in rng.integers(0, 256, 24):
+            assert orc.L.orc_gfni_affine_byte(m, int(x)) == orc.gf_mul(c, int(x)), (c, int(x))
+        assert orc.L.orc_gfni_affine_byte(m, 1) == c and orc.L.orc_gfni_affine_byte(m, 0) == 0
+
+
+@pytest.mark.skipif(not oracle.have_ref(), reason="oracle/_ref not built here")
+@pytest.mark.parametrize("kind", ["base", "avx2", "avx512", "gfni"])
+def test_kernel_families_vs_ref_random_sweep(orc, kind):
+    """Every family's ec_encode_data, with its own table format, equals the
+    reference's ec_encode_data_base (oracle/_ref) byte for byte; lengths
+    cover the < 64 scalar path, the overlapped last vector and several
+    threads. On a CPU without the ISA the scalar model runs (and says so)."""
+    ref = oracle.RefIsal()
+    rng = np.random.default_rng(11)
+    for it in range(40):
+        k = int(rng.integers(1, 60))
+        m = int(rng.integers(1, 14))
+        ln = int(rng.integers(1, 1500)) if it % 4 else int(rng.integers(8192, 20000))
+        mat = ref.cauchy1(k + m, k)[k:]
+        data = [rng.integers(0, 256, ln, dtype=np.uint8) for _ in range(k)]
+        want = ref.encode_data(ref.init_tables(k, m, mat), data, m)
+        tb = orc.init_tables_kind(kind, k, m, mat)
+        for threads in (1, 3):
+            got = orc.encode_data_kind(kind, tb, data, m, threads=threads)
+            assert all(np.array_equal(a, b) for a, b in zip(got, want)), (kind, k, m, ln, threads)
+
+
+@pytest.mark.parametrize("kind", ["avx512", "gfni"])
+def test_codec_encode_golden_kernel_families(orc, manifest, kind):
+    """The whole encodeData flow (global rows + per-group passes, XOR and
+    literal modes) on the AVX-512 / GFNI families against the golden
+    vectors made from oracle/_ref."""
+    for e in manifest["encode"]:
+        c = orc.codec(e["code_type"], e["k"], e["m"], max(e["r"], 1) if e["code_type"] in "CL" else e["r"], e["len"])
+        data = [orc.fill(e["len"], e["seed"], 0, j) for j in range(e["k"])]
+        got = c.encode(data, kind=kind)
+        want = golden_blocks(e["xor"], len(got), e["len"])
+        assert all(np.array_equal(g, w) for g, w in zip(got, want)), (e["name"], kind)
+        assert [sha(x) for x in c.encode(data, literal=True, kind=kind, threads=2)] == e["literal_sha256"]
+
+
+def test_isal_master_dispatch_rule(orc):
+    """ISA-L master picks AVX-512 + GFNI, else AVX-512, else AVX2, else base."""
+    order = [x for x in ("gfni", "avx512", "avx2") if orc.have_kind(x)]
+    assert orc.isal_master_kind() == (order[0] if order else "base")
