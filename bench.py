@@ -109,7 +109,7 @@ def parse(argv=None):
                          "exits (a rank stuck in a GPU call included)")
     ap.add_argument("--collective-timeout", type=float, default=120.0,
                     help="seconds a leg collective waits for the other ranks before the group counts as broken")
-    ap.add_argument("--profile-csv", default=os.path.join(REPO, "profiles", "r06fin_bench_kernel_stats.csv"),
+    ap.add_argument("--profile-csv", default=os.path.join(REPO, "profiles", "r06a_bench_kernel_stats.csv"),
                     help="committed rocprofv3 --stats kernel summary of this workload on this kernel build: the "
                          "line's roofline.profile_frac / profile_repair_frac are recomputed from it")
     ap.add_argument("--pageable", action="store_true",
@@ -276,6 +276,7 @@ class Dist:
             dist.all_reduce(t, group=self.pg)
         except Exception as e:  # timeout (a rank hung) or closed connection (a rank died)
             self.broken = f"collective failed in leg {self.leg}: {type(e).__name__}: {str(e)[:240]}"
+            self.touch("abort")  # tells a rank 0 stuck in a GPU call to print (Line._watch)
             raise GroupBroken(self.broken) from None
         if t[0] > 0 and not fail:
             raise LegAborted(int(t[0].item()))
@@ -302,6 +303,7 @@ class Dist:
             dist.all_gather_object(out, obj, group=self.pg)
         except Exception as e:
             self.broken = f"collective failed after leg {self.leg}: {type(e).__name__}: {str(e)[:240]}"
+            self.touch("abort")
             raise GroupBroken(self.broken) from None
         return out
 
@@ -364,6 +366,26 @@ class Dist:
         first = failed[0] if failed else None
         return None, {"error": errs[first] if failed else "aborted", "rank": first, "failed_ranks": failed}
 
+    def marker(self, what: str) -> str | None:
+        """Path of this run's marker file `what` ("abort": a rank's collective
+        failed; "printed": rank 0 printed the line), shared by the ranks of
+        one launch (same host, same rendezvous); None at N = 1."""
+        if self.world == 1:
+            return None
+        import tempfile
+
+        tag = "_".join(os.environ.get(x, "") for x in ("MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID"))
+        return os.path.join(tempfile.gettempdir(), f"ecw_bench_{tag.replace('/', '_')}.{what}")
+
+    def touch(self, what: str):
+        path = self.marker(what)
+        if path:
+            try:
+                with open(path, "a") as f:
+                    f.write(f"{self.rank} {time.time():.3f}\n")
+            except OSError:
+                pass
+
     def _free_device(self):
         if not self.dry:
             import gc
@@ -386,13 +408,20 @@ class Dist:
 class Line:
     """Rank 0's one JSON line. The legs fill it in as they finish; it is
     printed exactly once: at the end, or -- with whatever is in it and an
-    `error` -- when the hard deadline (--deadline-s after the process started)
-    passes or the launcher sends SIGTERM (torch.distributed.run does when
-    another rank exits non-zero). A watchdog thread does the last two, so a
-    rank stuck inside a GPU call still gets its line out; every other rank
-    just exits at its deadline."""
+    `error` -- by a watchdog thread (so a rank stuck inside a GPU call still
+    gets its line out) when
+      * the hard deadline passes (--deadline-s after the process started),
+      * the launcher sends SIGTERM (torch.distributed.run does when another
+        rank exits non-zero), or
+      * another rank's collective failed (its "abort" marker) and rank 0 has
+        not printed --collective-timeout + 30 s later (rank 0 is the stuck one).
+    Every other rank exits at its deadline, or 15 s after rank 0 printed (its
+    "printed" marker) if it is still running then (a hung rank), so a hang
+    never holds the launcher until the deadline."""
 
-    def __init__(self, d: Dist, deadline_s: float):
+    GRACE_AFTER_PRINT_S = 15.0
+
+    def __init__(self, d: Dist, deadline_s: float, collective_timeout: float = 120.0):
         import signal
         import threading
 
@@ -400,6 +429,7 @@ class Line:
         self.lock = threading.Lock()
         self.d = d
         self.deadline = T_START + deadline_s + (0.0 if d.rank == 0 else 5.0)  # rank 0 prints first
+        self.abort_grace = collective_timeout + 30.0
         r, w = os.pipe()
         os.set_blocking(w, False)
         signal.signal(signal.SIGTERM, lambda *_: None)  # the watchdog acts on it (set_wakeup_fd)
@@ -407,21 +437,40 @@ class Line:
         self._r = r
         threading.Thread(target=self._watch, daemon=True, name="bench-watchdog").start()
 
+    @staticmethod
+    def _age(path: str | None) -> float | None:
+        try:
+            return time.time() - os.path.getmtime(path) if path else None
+        except OSError:
+            return None
+
     def _watch(self):
         import select
 
+        leg = lambda: self.d.leg or "(between legs)"  # noqa: E731
         while True:
             left = self.deadline - time.time()
             if left <= 0:
-                why = (f"hard deadline: {self.deadline - T_START:.0f} s after start, still in leg "
-                       f"{self.d.leg or '(between legs)'}")
+                why = f"hard deadline: {self.deadline - T_START:.0f} s after start, still in leg {leg()}"
                 break
-            ready, _, _ = select.select([self._r], [], [], left)
+            ready, _, _ = select.select([self._r], [], [], min(1.0, left))
             if ready:
                 os.read(self._r, 64)
-                why = (f"terminated by the launcher (SIGTERM: another rank exited) in leg "
-                       f"{self.d.leg or '(between legs)'}")
+                why = f"terminated by the launcher (SIGTERM: another rank exited) in leg {leg()}"
                 break
+            if self.d.world > 1:
+                if self.rank != 0:
+                    age = self._age(self.d.marker("printed"))
+                    if age is not None and age > self.GRACE_AFTER_PRINT_S:
+                        print(f"bench.py: rank {self.rank} still in leg {leg()} {age:.0f} s after rank 0 printed the "
+                              f"line: exiting", file=sys.stderr, flush=True)
+                        os._exit(0)
+                elif not self.printed:
+                    age = self._age(self.d.marker("abort"))
+                    if age is not None and age > self.abort_grace:
+                        why = (f"rank 0 stuck in leg {leg()}: another rank's collective failed {age:.0f} s ago "
+                               f"(a rank hung or died)")
+                        break
         if self.rank == 0:
             self.emit(error=why)
         os._exit(0)
@@ -457,6 +506,7 @@ class Line:
             line["leg_seconds"] = dict(self.d.leg_seconds)
             sys.stdout.write(json.dumps(line, default=str) + "\n")
             sys.stdout.flush()
+            self.d.touch("printed")
 
 
 def plan(args, d: Dist, free_bytes: int, parity_num: int, fill: bool = False) -> dict:
@@ -1536,7 +1586,7 @@ def leg_estimates(args, world: int) -> dict:
         "configs4": 40.0,            # fill + time + verify a ~280 GB slab
         "configs1": 12.0, "configs0_shape": 12.0,
         "host_resident": 25.0 + 3.0 * world,  # pinned NUMA-local staging of 8.6 GiB per rank
-        "cpu_baseline": (c * (1 + 2 / 2 + 2 * (1 / 3 + 1 / 4)) + 15.0) if world == 1 else 0.0,
+        "cpu_baseline": (5.5 * c + 10.0) if world == 1 else 0.0,  # r06a: 65.7 s at --cpu-seconds 12
         "chunk_generator": 20.0 + (c / 4 if world == 1 else 0.0),
     }
 
@@ -1639,7 +1689,7 @@ def main():
         small_calls(args)
         return
     d = Dist(args)
-    line = Line(d, args.deadline_s)
+    line = Line(d, args.deadline_s, args.collective_timeout)
     rc = 1
     try:
         rc = run_legs(args, d, line)

@@ -13,7 +13,8 @@ stripes. Three layouts:
   one after it (ecw_encode_batch_split_dev). Parity rows interleaved with the
   data rows at one stride (the "blocks" slab) cost the encode ~10 %; in a
   region of their own the block layout encodes at the tiled slab's rate
-  (tools/rw_layout.py).
+  (the study, tools/rw_layout.py, is in git history:
+  `git show 2666ebe:tools/rw_layout.py`).
 * ``"tiled"``: every block is cut into ``chunk``-byte column pieces (default
   ``default_chunk(k)``: 8 KiB, 16 KiB at k <= 32); piece c
   of the k data blocks of stripe s is one contiguous run of k * chunk bytes

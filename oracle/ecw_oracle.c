@@ -125,9 +125,13 @@ void orc_encode_data_base(int len, int srcs, int dests, const uint8_t* v, uint8_
 
 /* ---- AVX2 4-bit split port (the reference's actual CPU kernel family) ---- */
 #if defined(__x86_64__)
-__attribute__((target("avx2"))) static void dot_prod_avx2_rows(int len, int srcs, int rows,
-                                                                const uint8_t* v, uint8_t** src,
-                                                                uint8_t** dest) {
+/* rows is a compile-time constant at every call (dot_prod_avx2_rows below), so
+ * the accumulators live in registers as in the asm kernels */
+__attribute__((target("avx2"), always_inline)) static inline void dot_prod_avx2_n(int len, int srcs,
+                                                                                 const int rows,
+                                                                                 const uint8_t* v,
+                                                                                 uint8_t** src,
+                                                                                 uint8_t** dest) {
   /* rows <= 6 outputs per pass, as gf_{1..6}vect_dot_prod_avx2 */
   const __m256i mask = _mm256_set1_epi8(0x0f);
   int pos = 0;
@@ -154,6 +158,21 @@ __attribute__((target("avx2"))) static void dot_prod_avx2_rows(int len, int srcs
     if (pos == len - 32) break;
     pos += 32;
   }
+}
+
+#define ORC_ROWS_SWITCH(fn, rows, ...)         \
+  switch (rows) {                              \
+    case 1: fn(__VA_ARGS__, 1, v, src, dest); break; \
+    case 2: fn(__VA_ARGS__, 2, v, src, dest); break; \
+    case 3: fn(__VA_ARGS__, 3, v, src, dest); break; \
+    case 4: fn(__VA_ARGS__, 4, v, src, dest); break; \
+    case 5: fn(__VA_ARGS__, 5, v, src, dest); break; \
+    default: fn(__VA_ARGS__, 6, v, src, dest); break; \
+  }
+
+__attribute__((target("avx2"))) static void dot_prod_avx2_rows(int len, int srcs, int rows, const uint8_t* v,
+                                                                uint8_t** src, uint8_t** dest) {
+  ORC_ROWS_SWITCH(dot_prod_avx2_n, rows, len, srcs)
 }
 
 static int have_avx2(void) {
@@ -230,9 +249,8 @@ uint8_t orc_gfni_affine_byte(uint64_t m, uint8_t x) {
 }
 
 #if defined(__x86_64__)
-__attribute__((target("avx512f,avx512bw"))) static void dot_prod_avx512_rows(int len, int srcs, int rows,
-                                                                             const uint8_t* v, uint8_t** src,
-                                                                             uint8_t** dest) {
+__attribute__((target("avx512f,avx512bw"), always_inline)) static inline void dot_prod_avx512_n(
+    int len, int srcs, const int rows, const uint8_t* v, uint8_t** src, uint8_t** dest) {
   const __m512i mask = _mm512_set1_epi8(0x0f);
   int pos = 0;
   for (;;) {
@@ -260,9 +278,8 @@ __attribute__((target("avx512f,avx512bw"))) static void dot_prod_avx512_rows(int
   }
 }
 
-__attribute__((target("avx512f,avx512bw,gfni"))) static void dot_prod_gfni_rows(int len, int srcs, int rows,
-                                                                                const uint8_t* v, uint8_t** src,
-                                                                                uint8_t** dest) {
+__attribute__((target("avx512f,avx512bw,gfni"), always_inline)) static inline void dot_prod_gfni_n(
+    int len, int srcs, const int rows, const uint8_t* v, uint8_t** src, uint8_t** dest) {
   int pos = 0;
   for (;;) {
     if (pos > len - 64) {
@@ -283,6 +300,18 @@ __attribute__((target("avx512f,avx512bw,gfni"))) static void dot_prod_gfni_rows(
     if (pos == len - 64) break;
     pos += 64;
   }
+}
+
+__attribute__((target("avx512f,avx512bw"))) static void dot_prod_avx512_rows(int len, int srcs, int rows,
+                                                                             const uint8_t* v, uint8_t** src,
+                                                                             uint8_t** dest) {
+  ORC_ROWS_SWITCH(dot_prod_avx512_n, rows, len, srcs)
+}
+
+__attribute__((target("avx512f,avx512bw,gfni"))) static void dot_prod_gfni_rows(int len, int srcs, int rows,
+                                                                                const uint8_t* v, uint8_t** src,
+                                                                                uint8_t** dest) {
+  ORC_ROWS_SWITCH(dot_prod_gfni_n, rows, len, srcs)
 }
 #endif
 

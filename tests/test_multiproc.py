@@ -304,14 +304,14 @@ def test_bench_injected_failure_mid_leg(n, rank, leg, at):
 def test_bench_hung_rank_times_out_and_line_survives():
     """A rank hanging inside a leg (as inside a GPU call): the others' leg
     collective times out (--collective-timeout), they skip the later
-    collective legs, rank 0 prints the line; the hung rank exits at its
-    deadline, so the launcher returns."""
+    collective legs, rank 0 prints the line; the hung rank exits soon after
+    the line is out (not at its deadline), so the launcher returns."""
     import time
 
     t0 = time.time()
     p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-fail", "rank=1,leg=configs1,at=1,mode=hang",
-                     "--collective-timeout", "4", "--deadline-s", "25")
-    assert time.time() - t0 < 120
+                     "--collective-timeout", "4", "--deadline-s", "200")
+    assert time.time() - t0 < 60
     assert p.returncode == 0, p.stderr[-2000:]
     _main_intact(line, 2)
     assert "collective failed in leg configs1" in line["configs1"]["error"]
@@ -319,6 +319,23 @@ def test_bench_hung_rank_times_out_and_line_survives():
         assert "no collectives after an earlier failure" in line[leg]["skipped"]
     assert line["legs_not_measured"] == ["configs1", "configs0_shape", "host_resident"]
     assert "configs4" in line and "error" not in line["configs4"]
+    assert "after rank 0 printed the line: exiting" in p.stderr
+
+
+def test_bench_hung_rank0_prints_from_watchdog():
+    """Rank 0 itself stuck in a leg: the other rank's collective times out and
+    leaves an abort marker; rank 0's watchdog prints the line it has (the
+    main leg) --collective-timeout + 30 s later, well before the deadline."""
+    import time
+
+    t0 = time.time()
+    p, line = _bench("--gpus", "2", "--dry-run", "--dry-run-fail", "rank=0,leg=configs0_shape,at=1,mode=hang",
+                     "--collective-timeout", "4", "--deadline-s", "200")
+    assert time.time() - t0 < 90
+    assert p.returncode == 0, p.stderr[-2000:]
+    _main_intact(line, 2)
+    assert "rank 0 stuck in leg configs0_shape" in line["error"]
+    assert "configs0_shape" in line["legs_not_measured"] and "stripes_per_gpu" in line["configs1"]
 
 
 def test_bench_rank_exit_still_prints_line():
