@@ -98,6 +98,8 @@ def parse(argv=None):
                     help="no GPU: plan every rank's share and run the rank orchestration and timing reduction "
                          "only (CPU test of the N>1 path; --dry-run-free-gib stands in for free HBM)")
     ap.add_argument("--dry-run-free-gib", type=float, default=287.0)
+    ap.add_argument("--dry-run-slow", type=float, default=1.0,
+                    help="--dry-run: scale the stand-in legs' sleeps (a longer run for the orchestration tests)")
     ap.add_argument("--inject-fail", "--dry-run-fail", dest="inject_fail", default=None,
                     help="rank=R,leg=NAME[,at=I][,mode=raise|hang|exit]: make rank R fail in leg NAME (at its start, "
                          "or just before the leg's I-th collective) -- the test of the fail-safe N>1 path")
@@ -195,6 +197,7 @@ class Dist:
         self.leg, self.leg_sync, self.broken = None, 0, None
         self.leg_seconds = {}
         self.dev, self.ndev, self.backend, self.pg = None, 0, None, None
+        self.run_tag = None
         if not self.dry:
             import torch
 
@@ -221,6 +224,10 @@ class Dist:
             dist.init_process_group("gloo", timeout=datetime.timedelta(seconds=max(600.0, args.collective_timeout)))
             self.pg = dist.new_group(backend="gloo", timeout=datetime.timedelta(seconds=args.collective_timeout))
             self.backend = dist.get_backend()
+            # this launch's marker-file tag (Line._watch): rank 0's pid and start time,
+            # so a later launch on the same host and port never sees this one's files
+            pid0, t0 = self._sync(float(os.getpid()))[0], self._sync(T_START)[0]
+            self.run_tag = f"{int(pid0)}_{int(t0 * 1000)}"
             if not self.dry:
                 # one process per GPU: which physical GPU each rank drives (PCI
                 # domain / bus / device), so the line is right whether every rank
@@ -367,15 +374,16 @@ class Dist:
         return None, {"error": errs[first] if failed else "aborted", "rank": first, "failed_ranks": failed}
 
     def marker(self, what: str) -> str | None:
-        """Path of this run's marker file `what` ("abort": a rank's collective
+        """Path of this launch's marker file `what` ("abort": a rank's collective
         failed; "printed": rank 0 printed the line), shared by the ranks of
-        one launch (same host, same rendezvous); None at N = 1."""
+        one launch (same host; tagged with rank 0's pid and start time, so
+        launches one after another on one port never share one); None at N = 1."""
         if self.world == 1:
             return None
         import tempfile
 
-        tag = "_".join(os.environ.get(x, "") for x in ("MASTER_ADDR", "MASTER_PORT", "TORCHELASTIC_RUN_ID"))
-        return os.path.join(tempfile.gettempdir(), f"ecw_bench_{tag.replace('/', '_')}.{what}")
+        tag = f"{os.environ.get('MASTER_PORT', '')}_{self.run_tag}"
+        return os.path.join(tempfile.gettempdir(), f"ecw_bench_{tag}.{what}")
 
     def touch(self, what: str):
         path = self.marker(what)
@@ -1225,10 +1233,13 @@ def dry_main(args, d: Dist) -> dict:
                        for a, b, c, o in zip(*shares)]}
 
 
+DRY_SLOW = [1.0]  # --dry-run-slow
+
+
 def dry_timed(d: Dist, unit_s: float) -> float:
     d.barrier()
     t0 = time.perf_counter()
-    time.sleep(unit_s * (1 + d.rank))
+    time.sleep(unit_s * DRY_SLOW[0] * (1 + d.rank))
     d.barrier()
     return time.perf_counter() - t0
 
@@ -1688,6 +1699,7 @@ def main():
     if args.small_calls:
         small_calls(args)
         return
+    DRY_SLOW[0] = args.dry_run_slow
     d = Dist(args)
     line = Line(d, args.deadline_s, args.collective_timeout)
     rc = 1

@@ -368,3 +368,27 @@ def test_bench_n8_estimate_within_budget():
     assert b["estimated_total_s"] < b["budget_s"] < b["deadline_s"] <= 540
     assert set(b["estimate_s"]) == {"configs4", "configs1", "configs0_shape", "host_resident", "chunk_generator"}
     assert line["legs_not_measured"] == []
+
+
+def test_bench_launches_on_one_port_do_not_share_markers():
+    """The driver runs N = 1, 2, 4, 8 back to back, possibly on one master
+    port: a later launch must not read an earlier launch's "printed" marker
+    (its ranks would take it as rank 0 having printed and exit)."""
+    import json
+    import subprocess
+    import sys
+    import time
+
+    port = _free_port()
+    e = {x: v for x, v in os.environ.items() if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr",
+           "127.0.0.1", f"--master-port={port}", os.path.join(REPO, "bench.py"), "--gpus", "2", "--dry-run",
+           "--dry-run-slow", "20"]  # a run of several seconds: the watchdog polls every second
+    lines = []
+    for i in range(2):
+        p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=e)
+        assert p.returncode == 0, p.stderr[-2000:]
+        lines.append(json.loads([x for x in p.stdout.splitlines() if x.startswith("{")][0]))
+        if i == 0:
+            time.sleep(17)  # older than Line.GRACE_AFTER_PRINT_S
+    assert lines[1]["legs_not_measured"] == [] and "rank_GBps" in lines[1]["host_resident"]
