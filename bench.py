@@ -395,13 +395,19 @@ class Dist:
                 pass
 
     def _free_device(self):
+        """Return a finished leg's HBM to the device (never raises: after a GPU
+        fault on this rank the context may refuse, and the next legs fail and
+        abort on their own)."""
         if not self.dry:
-            import gc
+            try:
+                import gc
 
-            import torch
+                import torch
 
-            gc.collect()
-            torch.cuda.empty_cache()
+                gc.collect()
+                torch.cuda.empty_cache()
+            except Exception as e:  # noqa: BLE001
+                print(f"bench.py: rank {self.rank}: freeing device memory failed: {e}", file=sys.stderr)
 
     def close(self):
         if self.world > 1:
