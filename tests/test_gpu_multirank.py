@@ -72,3 +72,31 @@ def test_two_ranks_union_equals_single_process(tmp_path, mode):
         assert np.array_equal(got_par[s], want_orc[s]), (mode, s)
         assert np.array_equal(got_par[s], want[s]), (mode, s)
         assert np.array_equal(got_rep[s], d0[s]), (mode, s)
+
+
+def test_bench_two_ranks_survive_an_injected_failure():
+    """bench.py's fail-safe N > 1 path with the product on the GPU (both ranks on
+    the box's one GPU): rank 1 raises in the middle of the configs1 leg, after
+    its second collective; every rank leaves that leg at the same collective,
+    the line keeps the main leg (verified against the oracle) and every other
+    leg, and names the failing rank."""
+    import json
+
+    REPO = os.path.dirname(HERE)
+    env = {x: v for x, v in os.environ.items() if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    cmd = [sys.executable, os.path.join(REPO, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--block-mib", "4", "--stripes", "2", "--configs4-steps", "0", "--shape-steps", "1",
+           "--other-layout-steps", "0", "--host-iters", "1", "--cpu-seconds", "0",
+           "--inject-fail", "rank=1,leg=configs1,at=2", "--collective-timeout", "60"]
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode == 0, p.stderr[-3000:]
+    lines = [x for x in p.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["value"] > 0 and line["verified"] and line["n_gpus"] == 2
+    c1 = line["configs1"]
+    assert c1["rank"] == 1 and c1["failed_ranks"] == [1] and "before collective 2" in c1["error"]
+    assert line["configs0_shape"]["verified"] and line["host_resident"]["verified"]
+    assert line["chunk_generator"]["verified"]
+    assert line["legs_not_measured"] == ["configs1"]

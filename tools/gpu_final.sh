@@ -7,7 +7,10 @@
 # (-> pmc_traffic*.json via tools/prof_summary.py), configs[3] traced -- and
 # the N=2 hang rehearsal (a rank stops in a leg; the other's collective times
 # out; rank 0 still prints). Each GPU step has its own limit; the script stops
-# at the first failure.
+# at the first failure. PART=c: the N>1 orchestration with 4 real GPU
+# processes sharing the one GPU (16 MiB main-leg blocks so four ranks fit),
+# plain, with a rank hanging in a leg and with a rank exiting mid-leg -- the
+# line must come out every time -- and the new 2-rank GPU test.
 # Run: gpurun -- 'TAG=r06a PART=a bash tools/gpu_final.sh'
 set -uo pipefail
 cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out && export TMPDIR=/tmp
@@ -39,4 +42,15 @@ if [ "${PART:-a}" = b ]; then
   cd $R
   timeout -k 10 400 python bench.py --gpus 2 --steps 10 --configs4-steps 2 --shape-steps 2 --other-layout-steps 0 --inject-fail rank=1,leg=configs1,at=1,mode=hang --collective-timeout 20 --deadline-s 240 > $O/bench_2rank_hang.log 2>&1 || { tail -20 $O/bench_2rank_hang.log; exit 1; }
   tail -1 $O/bench_2rank_hang.log | cut -c1-300
+fi
+if [ "${PART:-a}" = c ]; then
+  timeout -k 10 300 python -u -m pytest tests/test_gpu_multirank.py -x -v --timeout 280 --timeout-method thread -p no:cacheprovider > $O/pytest_multirank.log 2>&1 || { tail -40 $O/pytest_multirank.log; exit 1; }
+  tail -2 $O/pytest_multirank.log
+  Q="--block-mib 16 --steps 10 --configs4-steps 2 --shape-steps 2 --other-layout-steps 0"
+  timeout -k 10 400 python bench.py --gpus 4 $Q > $O/bench_4rank.log 2>&1 || { tail -20 $O/bench_4rank.log; exit 1; }
+  tail -1 $O/bench_4rank.log | cut -c1-300
+  timeout -k 10 400 python bench.py --gpus 4 $Q --inject-fail rank=2,leg=configs0_shape,at=1,mode=hang --collective-timeout 30 > $O/bench_4rank_hang.log 2>&1 || { tail -20 $O/bench_4rank_hang.log; exit 1; }
+  tail -1 $O/bench_4rank_hang.log | cut -c1-300
+  timeout -k 10 400 python bench.py --gpus 4 $Q --inject-fail rank=3,leg=configs4,at=2,mode=exit > $O/bench_4rank_exit.log 2>&1; echo "exit-mode rc=$?"
+  tail -1 $O/bench_4rank_exit.log | cut -c1-300
 fi
