@@ -440,6 +440,7 @@ class Line:
         import threading
 
         self.rank, self.data, self.printed = d.rank, {}, False
+        self.expected = []  # the optional legs this run meant to measure (run_legs)
         self.lock = threading.Lock()
         self.d = d
         self.deadline = T_START + deadline_s + (0.0 if d.rank == 0 else 5.0)  # rank 0 prints first
@@ -514,8 +515,10 @@ class Line:
                    and ("error" in line[x] or "skipped" in line[x])]
             if "main_error" in line or line.get("value") is None and not line.get("dry_run"):
                 bad = ["main"] + bad
-            if error and self.d.leg:
+            if error and self.d.leg and self.d.leg not in bad:
                 bad.append(self.d.leg)
+            # legs the run meant to measure that never reached the line (cut off by `error`)
+            bad += [x for x in self.expected if x not in line and x not in bad]
             line["legs_not_measured"] = bad
             line["leg_seconds"] = dict(self.d.leg_seconds)
             sys.stdout.write(json.dumps(line, default=str) + "\n")
@@ -1623,6 +1626,8 @@ def run_legs(args, d: Dist, line: Line) -> int:
         "cpu_baseline": args.cpu_seconds > 0 and d.world == 1,
         "chunk_generator": args.host_iters > 0,
     }
+    line.expected = [x for x in LEG_NAMES if x != "main" and enabled.get(x)
+                     and (d.rank == 0 or x not in ("cpu_baseline", "chunk_generator"))]
     E = None
     if not d.dry:
         import ecwide_amd as E

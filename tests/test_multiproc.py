@@ -345,7 +345,10 @@ def test_bench_rank_exit_still_prints_line():
                      "--collective-timeout", "20")
     assert line is not None, p.stderr[-2000:]
     _main_intact(line, 2)
-    assert "in leg configs4" in line["error"] and "configs4" in line["legs_not_measured"]
+    assert "in leg configs4" in line["error"] or "(between legs)" in line["error"]
+    # every leg after the cut is listed, the one in flight included
+    assert {"configs4", "configs1", "configs0_shape", "host_resident", "chunk_generator"} <= set(
+        line["legs_not_measured"])
 
 
 def test_bench_time_budget_drops_optional_legs():
