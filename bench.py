@@ -111,7 +111,7 @@ def parse(argv=None):
                          "exits (a rank stuck in a GPU call included)")
     ap.add_argument("--collective-timeout", type=float, default=120.0,
                     help="seconds a leg collective waits for the other ranks before the group counts as broken")
-    ap.add_argument("--profile-csv", default=os.path.join(REPO, "profiles", "r06a_bench_kernel_stats.csv"),
+    ap.add_argument("--profile-csv", default=os.path.join(REPO, "profiles", "r06fin_bench_kernel_stats.csv"),
                     help="committed rocprofv3 --stats kernel summary of this workload on this kernel build: the "
                          "line's roofline.profile_frac / profile_repair_frac are recomputed from it")
     ap.add_argument("--pageable", action="store_true",
