@@ -56,3 +56,19 @@ def test_host_paths_clean_under_asan_ubsan():
     assert p.returncode == 0, tail
     assert "Sanitizer" not in p.stderr and "runtime error" not in p.stderr, tail
     assert " 0 failed" in p.stdout, tail
+
+
+def test_oracle_families_clean_under_asan_ubsan():
+    """The checker too: oracle/ecw_oracle.c's kernel families (the CPU
+    baseline's AVX2 / AVX-512 / GFNI ports) equal ec_encode_data_base on
+    random shapes and ragged lengths, with no sanitizer report."""
+    exe = os.path.join(OUT, "oracle_asan")
+    os.makedirs(OUT, exist_ok=True)
+    subprocess.run(["gcc", "-O1", "-g", "-fsanitize=address,undefined", "-fno-sanitize-recover=undefined",
+                    "-fno-omit-frame-pointer", os.path.join(REPO, "tests", "csrc", "asan_oracle.c"),
+                    os.path.join(REPO, "oracle", "ecw_oracle.c"), "-lpthread", "-o", exe], check=True)
+    p = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1"))
+    tail = (p.stdout + p.stderr)[-4000:]
+    assert p.returncode == 0 and "asan oracle ok" in p.stdout, tail
+    assert "runtime error" not in p.stderr, tail
