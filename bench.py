@@ -461,6 +461,7 @@ class Line:
 
     def _watch(self):
         import select
+        import signal
 
         leg = lambda: self.d.leg or "(between legs)"  # noqa: E731
         while True:
@@ -469,8 +470,8 @@ class Line:
                 why = f"hard deadline: {self.deadline - T_START:.0f} s after start, still in leg {leg()}"
                 break
             ready, _, _ = select.select([self._r], [], [], min(1.0, left))
-            if ready:
-                os.read(self._r, 64)
+            # the wakeup fd carries one byte per signal number; only SIGTERM is ours
+            if ready and int(signal.SIGTERM) in os.read(self._r, 64):
                 why = f"terminated by the launcher (SIGTERM: another rank exited) in leg {leg()}"
                 break
             if self.d.world > 1:
