@@ -472,7 +472,8 @@ class Line:
             ready, _, _ = select.select([self._r], [], [], min(1.0, left))
             # the wakeup fd carries one byte per signal number; only SIGTERM is ours
             if ready and int(signal.SIGTERM) in os.read(self._r, 64):
-                why = f"terminated by the launcher (SIGTERM: another rank exited) in leg {leg()}"
+                why = (f"terminated (SIGTERM) in leg {leg()}"
+                       + ("; torch.distributed.run sends it when another rank exits" if self.d.world > 1 else ""))
                 break
             if self.d.world > 1:
                 if self.rank != 0:
@@ -487,9 +488,11 @@ class Line:
                         why = (f"rank 0 stuck in leg {leg()}: another rank's collective failed {age:.0f} s ago "
                                f"(a rank hung or died)")
                         break
+        rc = 0
         if self.rank == 0:
             self.emit(error=why)
-        os._exit(0)
+            rc = 0 if self.data.get("value") is not None or self.data.get("dry_run") else 1
+        os._exit(rc)  # as main(): 0 whenever the line carries the main leg's `value`
 
     def update(self, **kv):
         with self.lock:
@@ -1629,6 +1632,8 @@ def run_legs(args, d: Dist, line: Line) -> int:
     }
     line.expected = [x for x in LEG_NAMES if x != "main" and enabled.get(x)
                      and (d.rank == 0 or x not in ("cpu_baseline", "chunk_generator"))]
+    # the line's frame from the start, so a line cut off inside the main leg still says what it is
+    line.update(metric=METRIC, value=None, unit="GB/s", n_gpus=d.world)
     E = None
     if not d.dry:
         import ecwide_amd as E

@@ -345,7 +345,7 @@ def test_bench_rank_exit_still_prints_line():
                      "--collective-timeout", "20")
     assert line is not None, p.stderr[-2000:]
     _main_intact(line, 2)
-    assert "in leg configs4" in line["error"] or "(between legs)" in line["error"]
+    assert "SIGTERM" in line["error"] and ("in leg configs4" in line["error"] or "(between legs)" in line["error"])
     # every leg after the cut is listed, the one in flight included
     assert {"configs4", "configs1", "configs0_shape", "host_resident", "chunk_generator"} <= set(
         line["legs_not_measured"])
@@ -395,3 +395,48 @@ def test_bench_launches_on_one_port_do_not_share_markers():
         if i == 0:
             time.sleep(17)  # older than Line.GRACE_AFTER_PRINT_S
     assert lines[1]["legs_not_measured"] == [] and "rank_GBps" in lines[1]["host_resident"]
+
+
+def test_bench_sigterm_at_n1_prints_the_line():
+    """A launcher's SIGTERM (or a driver's own time limit) in the middle of a
+    run: the watchdog prints the line it has, with the leg it was in, once."""
+    import json
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    e = {x: v for x, v in os.environ.items() if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--dry-run-slow", "200"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e)
+    time.sleep(15)  # the stand-in main leg takes 10 s at this scale, configs4 4 s more
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=60)
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, (out[-2000:], err[-2000:])
+    line = json.loads(lines[0])
+    assert line["error"].startswith("terminated (SIGTERM) in leg") and line["n_gpus"] == 1
+    assert line["dry_run"] and "in leg main" not in line["error"]  # the main leg finished before the signal
+    assert p.returncode == 0  # the main leg (a dry run here) is in the line
+
+
+def test_bench_sigterm_inside_main_leg_fails_the_run():
+    """Cut off inside the main leg: one line that still names the metric, no
+    value, exit code 1."""
+    import json
+    import signal
+    import subprocess
+    import sys
+    import time
+
+    e = {x: v for x, v in os.environ.items() if x not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    p = subprocess.Popen([sys.executable, os.path.join(REPO, "bench.py"), "--dry-run", "--dry-run-slow", "400"],
+                         stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=e)
+    time.sleep(8)
+    p.send_signal(signal.SIGTERM)
+    out, err = p.communicate(timeout=60)
+    lines = [x for x in out.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, (out[-2000:], err[-2000:])
+    line = json.loads(lines[0])
+    assert line["metric"] and line["value"] is None and "in leg main" in line["error"]
+    assert line["legs_not_measured"][0] == "main" and p.returncode == 1
